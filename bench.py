@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident QPACK Huffman encode + decode throughput.
+
+Metric (BASELINE.json): GB/s of device-resident QPACK Huffman enc+dec on a
+1M-string batch per GPU.  One step = one encode pass over the rank's 1M-string
+synthetic batch (config 2) + one decode pass over the Huffman payload of a
+1M-string batch (config 3), both through the C-ABI (libqhuff.so).  value =
+(raw bytes encoded + raw bytes decoded, summed over ranks) / wall time.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU; strings are sharded, no
+collective on the data path: "scaling": "weak").
+
+Input buffers are rotated over --copies device copies (default 4, > 512 MB
+footprint) so a step does not re-read the previous step's bytes from the
+256 MB Infinity Cache.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ls-qpack_amd"))
+
+METRIC = ("GB/s device-resident QPACK Huffman enc+dec, 1M-string batch, "
+          "1/2/4/8 MI355X")
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=1 << 20,
+                    help="strings per GPU (default 1M)")
+    ap.add_argument("--copies", type=int, default=4)
+    ap.add_argument("--alphabet", default="token", choices=["token", "base64"])
+    ap.add_argument("--cpu-seconds", type=float, default=2.0,
+                    help="wall seconds per CPU-baseline leg (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = all usable cores, <= 16)")
+    ap.add_argument("--host-path", action="store_true",
+                    help="also time the PCIe-inclusive host-memory path")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
+                                                  "pmc_latest.json"),
+                    help="PMC traffic summary (tools/pmc_summary.py)")
+    return ap.parse_args()
+
+
+def usable_cores():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import qhuff
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    # ---- inputs: this rank's shard of an (world x n)-string batch --------------
+    alpha = (qhuff.TOKEN_ALPHABET if args.alphabet == "token"
+             else qhuff.BASE64_ALPHABET)
+    seed = 0x9E3779B97F4A7C15 ^ (rank * 0x632BE59BD9B4E019)
+    data, off = qhuff.synth_batch(args.n, seed=seed & 0xFFFFFFFFFFFFFFFF,
+                                  alphabet=alpha)
+    n = args.n
+    raw_bytes = int(off[-1])
+    codec = qhuff.Codec(local)
+
+    d_in = [torch.from_numpy(data).to(dev) for _ in range(args.copies)]
+    d_off = [torch.from_numpy(off.view(np.int32)).to(dev)
+             for _ in range(args.copies)]
+    enc_cap = qhuff.encode_bound(raw_bytes, n, 0)
+    e_out = [torch.empty(enc_cap, dtype=torch.uint8, device=dev)
+             for _ in range(args.copies)]
+    e_off = [torch.empty(n + 1, dtype=torch.int32, device=dev)
+             for _ in range(args.copies)]
+
+    # decode inputs = the Huffman payloads (forced Huffman), made once
+    h_out, h_off = codec.encode(d_in[0], d_off[0], 0)
+    torch.cuda.synchronize()
+    h_off_np = h_off.cpu().numpy().view(np.uint32)
+    huff_bytes = int(h_off_np[-1])
+    h_np = h_out[:huff_bytes].cpu().numpy()
+    del h_out
+    d_hin = [torch.from_numpy(h_np).to(dev) for _ in range(args.copies)]
+    d_hoff = [torch.from_numpy(h_off_np.view(np.int32)).to(dev)
+              for _ in range(args.copies)]
+    dec_cap = qhuff.decode_bound(huff_bytes, n)
+    d_out = [torch.empty(dec_cap, dtype=torch.uint8, device=dev)
+             for _ in range(args.copies)]
+    d_ooff = [torch.empty(n + 1, dtype=torch.int32, device=dev)
+              for _ in range(args.copies)]
+    d_st = [torch.empty(n, dtype=torch.uint8, device=dev)
+            for _ in range(args.copies)]
+
+    stream = torch.cuda.current_stream()
+
+    def step(i, ev=None):
+        k = i % args.copies
+        j = (i + args.copies // 2) % args.copies
+        if ev:
+            ev[0].record(stream)
+        codec.encode_into(d_in[k], d_off[k], n, 0, e_out[k], e_off[k], stream)
+        if ev:
+            ev[1].record(stream)
+        codec.decode_into(d_hin[j], d_hoff[j], n, d_out[j], d_ooff[j],
+                          d_st[j], stream)
+        if ev:
+            ev[2].record(stream)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+
+    # one correctness probe outside the timed region: round trip of copy 0
+    codec.decode_into(d_hin[0], d_hoff[0], n, d_out[0], d_ooff[0], d_st[0],
+                      stream)
+    torch.cuda.synchronize()
+    ok_dec = (torch.equal(d_out[0][:raw_bytes], d_in[0])
+              and bool((d_st[0] == 0).all())
+              and torch.equal(d_ooff[0], d_off[0]))
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    wall = t1 - t0
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+        okt = torch.tensor([1.0 if ok_dec else 0.0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok_dec = bool(okt.item() > 0.5)
+
+    ms_per_step = wall * 1e3 / args.steps
+    bytes_per_step = 2 * raw_bytes           # raw in (encode) + raw out (decode)
+    value = world * bytes_per_step / (wall / args.steps) / 1e9
+
+    # ---- roofline for the dominant kernel ---------------------------------------
+    alg_enc = raw_bytes + huff_bytes + 8 * n       # in, out, in_off, out_off
+    alg_dec = huff_bytes + raw_bytes + 9 * n       # + 1 B status
+    if dec_ms >= enc_ms:
+        kname, kms, alg = "qhuff_decode_tile", dec_ms, alg_dec
+    else:
+        kname, kms, alg = "qhuff_encode_tile", enc_ms, alg_enc
+    achieved = alg / (kms * 1e-3) / 1e9
+    traffic = None
+    pmc_src = None
+    if os.path.exists(args.pmc):
+        try:
+            pm = json.load(open(args.pmc))
+            ent = pm.get("kernels", {}).get(kname)
+            if ent and ent.get("n") == n:
+                traffic = ent.get("hbm_bytes_per_launch")
+                pmc_src = os.path.relpath(args.pmc, ROOT)
+        except Exception:
+            traffic = None
+    roof = {"bound": "hbm", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": kname, "kernel_us": round(kms * 1e3, 2),
+            "alg_bytes": alg}
+    if pmc_src:
+        roof["traffic_source"] = pmc_src
+
+    # ---- CPU baseline (rank 0, N = 1 only) -------------------------------------
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        threads = args.cpu_threads or usable_cores()
+
+        def leg(buf, offs, op, payload_bytes):
+            best, tot, reps = 1e30, 0.0, 0
+            while tot < args.cpu_seconds or reps < 2:
+                dt = oracle_lib.bench_pass(buf, offs, op, threads)
+                best = min(best, dt)
+                tot += dt
+                reps += 1
+            return payload_bytes / best / 1e9, reps
+
+        enc_gbs, r1 = leg(data, off, 0, raw_bytes)
+        dec_gbs, r2 = leg(h_np, h_off_np, 1, raw_bytes)
+        both = 2.0 / (1.0 / enc_gbs + 1.0 / dec_gbs)
+        cpu = {"value": round(both, 3), "unit": "GB/s", "cores": threads,
+               "kind": "port",
+               "sample": ("full %d-string batch, oracle restatement of "
+                          "lsqpack_enc_enc_str(7,..) + lsqpack_huff_decode "
+                          "(fast path), best of %d/%d passes, %d threads"
+                          % (n, r1, r2, threads)),
+               "enc_gbps": round(enc_gbs, 3), "dec_gbps": round(dec_gbs, 3)}
+
+    host = None
+    if args.host_path and rank == 0:
+        t = time.perf_counter()
+        e, eo = codec.encode_host(data, off, 0)
+        t_e = time.perf_counter() - t
+        t = time.perf_counter()
+        dd, do, st = codec.decode_host(h_np, h_off_np)
+        t_d = time.perf_counter() - t
+        host = {"enc_gbps": round(raw_bytes / t_e / 1e9, 3),
+                "dec_gbps": round(raw_bytes / t_d / 1e9, 3),
+                "note": "pinned hipMemcpyAsync in + kernel + out, synchronous"}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "GB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (xorshift64 %s alphabet, U[8,64] B strings)"
+                    % args.alphabet,
+            "config": {"workload": "config2+3: encode 1M strings + decode 1M "
+                                   "Huffman strings per GPU per step",
+                       "strings_per_gpu": n, "raw_bytes_per_gpu": raw_bytes,
+                       "huff_bytes_per_gpu": huff_bytes,
+                       "parallelism": "dp%d (independent string shards)" % world},
+            "enc_kernel_us": round(enc_ms * 1e3, 2),
+            "dec_kernel_us": round(dec_ms * 1e3, 2),
+            "enc_payload_gbps": round(raw_bytes / (enc_ms * 1e-3) / 1e9, 2),
+            "dec_payload_gbps": round(raw_bytes / (dec_ms * 1e-3) / 1e9, 2),
+            "roundtrip_ok": bool(ok_dec),
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        if host:
+            line["host_path"] = host
+        print(json.dumps(line), flush=True)
+    codec.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

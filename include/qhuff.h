@@ -1,0 +1,179 @@
+/*
+ * qhuff.h -- C-ABI of the MI355X-native QPACK Huffman string-literal codec.
+ *
+ * Drop-in boundary for the string-literal step of ls-qpack (v2.6.5).  The
+ * reference codes one string per synchronous call:
+ *
+ *   lsqpack_enc_enc_str()      lsqpack.c:839-876   (test/lsqpack-test.h:17-19)
+ *   qenc_enc_str_size()        lsqpack.c:5198-5210 (static; ratio guard 1946)
+ *   qenc_huffman_enc()         lsqpack.c:5085-5195 (static)
+ *   lsqpack_huff_decode()      lsqpack.c:3520-3535 (LSQPACK_DEVEL_MODE export)
+ *   lsqpack_huff_decode_full() lsqpack.c:3443-3517 (exported)
+ *
+ * This library codes a BATCH of independent strings per call on one GPU.
+ * Every entry point is plain C: pointers, sizes, status codes.  No HIP or
+ * torch types cross this header; `stream` is an opaque hipStream_t (NULL =
+ * the device's default stream).
+ *
+ * Batch layout (device memory unless a function says host):
+ *   in      strings packed back to back.
+ *   in_off  n + 1 uint32 exclusive offsets: string i is
+ *           in[in_off[i] .. in_off[i+1]).  in_off[0] need not be 0.
+ *   out     packed outputs; out_off (n + 1 entries) is written by the call:
+ *           output i is out[out_off[i] .. out_off[i+1]), out_off[0] = 0.
+ *
+ * Results are bit-exact with the reference functions named on each call.
+ * Failure is loud: a call returns a negative QHUFF_E* code, and the library
+ * has no CPU fallback -- without a usable gfx950 device qhuff_open fails.
+ */
+#ifndef QHUFF_H
+#define QHUFF_H 1
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QHUFF_ABI_VERSION 1
+
+/* return codes */
+#define QHUFF_OK          0
+#define QHUFF_EINVAL    (-22)   /* bad argument (NULL pointer, bad mode)   */
+#define QHUFF_ENOMEM    (-12)   /* device allocation failed                */
+#define QHUFF_ENODEV    (-19)   /* no usable device                        */
+#define QHUFF_ERANGE    (-34)   /* batch too large for 32-bit offsets      */
+#define QHUFF_EDEVICE   (-5)    /* a HIP call failed (see qhuff_last_error) */
+
+/* encode modes (qhuff_encode_batch `mode`) */
+#define QHUFF_ENC_PAYLOAD   0   /* qenc_huffman_enc output only (forced
+                                   Huffman, no framing), lsqpack.c:5085   */
+#define QHUFF_ENC_LITERAL3  3   /* lsqpack_enc_enc_str(3, ...) framing     */
+#define QHUFF_ENC_LITERAL5  5   /* lsqpack_enc_enc_str(5, ...)             */
+#define QHUFF_ENC_LITERAL7  7   /* lsqpack_enc_enc_str(7, ...)             */
+
+/* per-string decode status (qhuff_decode_batch `status`) */
+#define QHUFF_DEC_OK     0      /* HUFF_DEC_OK, lsqpack.c:3424             */
+#define QHUFF_DEC_ERROR  1      /* HUFF_DEC_ERROR, lsqpack.c:3427: EOS in
+                                   the data, padding > 7 bits, or padding
+                                   that is not the EOS prefix              */
+
+typedef struct qhuff_ctx qhuff_ctx;
+
+/* Open a codec context on HIP device `device` (one context per host thread
+ * per GPU).  Uploads the static Huffman tables once.  Calls on one context
+ * must be ordered on a single stream.  Returns QHUFF_OK or QHUFF_E*. */
+int qhuff_open(int device, qhuff_ctx **ctx_out);
+void qhuff_close(qhuff_ctx *ctx);
+
+/* Worst-case output bytes for an encode batch of n strings totalling
+ * in_bytes (30-bit longest code, + framing for LITERAL modes). */
+uint64_t qhuff_encode_bound(uint64_t in_bytes, uint32_t n, unsigned mode);
+
+/* Worst-case output bytes for a decode batch (5-bit shortest code,
+ * lsqpack.c:5072): floor(8 * in_bytes / 5). */
+uint64_t qhuff_decode_bound(uint64_t in_bytes, uint32_t n);
+
+/* Encode n strings (device pointers).
+ *   mode PAYLOAD: output i = qenc_huffman_enc(string i) (lsqpack.c:5085),
+ *                 exactly qenc_enc_str_size(string i) bytes (lsqpack.c:5198).
+ *   mode LITERAL3/5/7: output i = the bytes lsqpack_enc_enc_str(mode, dst,
+ *                 bound, string i) writes with dst[0] = 0 beforehand
+ *                 (lsqpack.c:839): H bit + prefixed length + Huffman, or
+ *                 H=0 + length + raw copy when Huffman is not shorter.
+ *                 Bits of byte 0 above the H bit are 0; the caller ORs its
+ *                 instruction bits in (as the reference's callers do).
+ * `out` must hold qhuff_encode_bound(...) bytes.  Asynchronous on `stream`. */
+int qhuff_encode_batch(qhuff_ctx *ctx, const uint8_t *in,
+                       const uint32_t *in_off, uint32_t n, unsigned mode,
+                       uint8_t *out, uint32_t *out_off, void *stream);
+
+/* Decode n complete Huffman strings (device pointers), with the semantics of
+ * lsqpack_huff_decode(src, len, dst, dst_len, &{resume 0}, final = 1)
+ * (lsqpack.c:3524-3529 -> huff_decode_fast, 5243) given a dst_len that
+ * cannot run out.  status[i] = QHUFF_DEC_OK or QHUFF_DEC_ERROR; an ERROR
+ * string contributes 0 output bytes.  `out` must hold
+ * qhuff_decode_bound(...) bytes.  Asynchronous on `stream`. */
+int qhuff_decode_batch(qhuff_ctx *ctx, const uint8_t *in,
+                       const uint32_t *in_off, uint32_t n, uint8_t *out,
+                       uint32_t *out_off, uint8_t *status, void *stream);
+
+/* Host-memory variants (PCIe-inclusive path: host -> pinned staging ->
+ * device -> kernel -> device -> pinned -> host).  Synchronous.  in_off and
+ * the returned out_off are host arrays of n + 1 entries; out must hold the
+ * corresponding bound.  *out_total receives out_off[n]. */
+int qhuff_encode_batch_host(qhuff_ctx *ctx, const uint8_t *in,
+                            const uint32_t *in_off, uint32_t n, unsigned mode,
+                            uint8_t *out, uint32_t *out_off);
+int qhuff_decode_batch_host(qhuff_ctx *ctx, const uint8_t *in,
+                            const uint32_t *in_off, uint32_t n, uint8_t *out,
+                            uint32_t *out_off, uint8_t *status);
+
+/* ---- per-string mirrors of the reference entry points -----------------
+ * Same argument meaning, return values and error behaviour as the reference
+ * functions; each call runs a one-string batch on the context's GPU (no CPU
+ * fallback).  Host pointers.  Synchronous. */
+
+/* lsqpack_enc_enc_str (lsqpack.c:839): returns bytes written or -1 when
+ * dst_len is too small.  Bits of dst[0] above prefix_bits+1 are kept. */
+int qhuff_enc_enc_str(qhuff_ctx *ctx, unsigned prefix_bits,
+                      unsigned char *dst, size_t dst_len,
+                      const unsigned char *str, unsigned str_len);
+
+/* qenc_enc_str_size (lsqpack.c:5198): Huffman size in bytes. */
+unsigned qhuff_enc_str_size(qhuff_ctx *ctx, const unsigned char *str,
+                            unsigned str_len);
+
+/* struct huff_decode_retval (lsqpack.c:3420-3431) */
+enum qhuff_huff_dec_status
+{
+    QHUFF_HUFF_DEC_OK,
+    QHUFF_HUFF_DEC_END_SRC,
+    QHUFF_HUFF_DEC_END_DST,
+    QHUFF_HUFF_DEC_ERROR
+};
+
+struct qhuff_decode_retval
+{
+    enum qhuff_huff_dec_status  status;
+    unsigned                    n_dst;
+    unsigned                    n_src;
+};
+
+/* lsqpack_huff_decode for a complete string (resume == 0 && final): OK with
+ * n_dst/n_src, ERROR with n_dst = n_src = 0 (lsqpack.c:5374-5425), or
+ * END_DST with n_dst = n_src = 0 when dst_len is too small (the reference
+ * may report partial progress there; callers grow dst and retry either way,
+ * lsqpack.c:3327-3365).  Chunked input (final = 0) is not a batch case and
+ * returns QHUFF_EINVAL through status ERROR. */
+struct qhuff_decode_retval
+qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, int src_len,
+                  unsigned char *dst, int dst_len);
+
+/* Last HIP error string for this context (diagnostics). */
+const char *qhuff_last_error(qhuff_ctx *ctx);
+
+/* ---- multi-GPU sharding helpers (host arithmetic only) ----------------
+ * Byte-balanced contiguous partition of a batch into g shards: writes
+ * g + 1 string indices to cuts (cuts[0] = 0, cuts[g] = n) so shard k holds
+ * strings [cuts[k], cuts[k+1]) with roughly equal input bytes
+ * (SURVEY.md section 8(e)). */
+int qhuff_shard_cuts(const uint32_t *in_off, uint32_t n, uint32_t g,
+                     uint32_t *cuts);
+
+/* Synthetic header-string batch: xorshift64
+ * seeded with `seed` (0 -> 0x9E3779B97F4A7C15); len = min_len +
+ * r % (max_len - min_len + 1); bytes alphabet[r % alphabet_len].  Host
+ * buffers: in_off gets n + 1 entries; data must hold n * max_len bytes.
+ * Returns the total bytes written. */
+uint64_t qhuff_synth_batch(uint64_t seed, uint32_t n, uint32_t min_len,
+                           uint32_t max_len, const uint8_t *alphabet,
+                           uint32_t alphabet_len, uint8_t *data,
+                           uint32_t *in_off);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,117 @@
+// qhuff_tables.cpp -- derive every table the kernels use from the RFC 7541
+// Appendix B code lengths (canonical Huffman: codes assigned in (length,
+// symbol) order).  Host code, run once per context.
+#include "qhuff_tables.h"
+
+#include <string.h>
+
+namespace qhuff {
+
+// RFC 7541 Appendix B code lengths, symbols 0..256 (EOS = 256).
+static const uint8_t kLen[257] = {
+    13,23,28,28,28,28,28,28,28,24,30,28,28,30,28,28,28,28,28,28,28,28,30,28,28,28,28,28,28,28,28,28,
+     6,10,10,12,13, 6, 8,11,10,10, 8,11, 8, 6, 6, 6, 5, 5, 5, 6, 6, 6, 6, 6, 6, 6, 7, 8,15, 6,12,10,
+    13, 6, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 8, 7, 8,13,19,13,14, 6,
+    15, 5, 6, 5, 6, 5, 6, 6, 6, 5, 7, 7, 6, 6, 6, 5, 6, 7, 6, 5, 5, 6, 7, 7, 7, 7, 7,15,11,14,13,28,
+    20,22,20,20,22,22,22,23,22,23,23,23,23,23,24,23,24,24,22,23,24,23,23,23,23,21,22,23,22,23,23,24,
+    22,21,20,22,22,23,23,21,23,22,22,24,21,22,23,23,21,21,22,21,23,22,23,23,20,22,22,22,23,22,22,23,
+    26,26,20,19,22,23,22,25,26,26,26,27,27,26,24,25,19,21,26,27,27,26,27,24,21,21,26,26,28,27,27,27,
+    20,24,20,21,22,21,21,23,22,22,25,25,24,24,26,23,26,27,26,26,27,27,27,27,27,28,27,27,27,27,27,26,
+    30,
+};
+
+namespace {
+
+struct Canon
+{
+    uint32_t first[31], count[31], base[31];
+    uint16_t sorted[257];
+};
+
+void
+canon_build(Canon *c, uint32_t *code)
+{
+    memset(c, 0, sizeof(*c));
+    for (int s = 0; s < 257; ++s)
+        c->count[kLen[s]]++;
+    uint32_t next = 0, idx = 0;
+    for (int L = 1; L <= 30; ++L)
+    {
+        next <<= 1;
+        c->first[L] = next;
+        c->base[L] = idx;
+        next += c->count[L];
+        idx += c->count[L];
+    }
+    uint32_t fill[31];
+    for (int L = 1; L <= 30; ++L)
+        fill[L] = 0;
+    for (int s = 0; s < 257; ++s)          // symbol order within a length
+    {
+        int L = kLen[s];
+        code[s] = c->first[L] + fill[L];
+        c->sorted[c->base[L] + fill[L]] = (uint16_t) s;
+        fill[L]++;
+    }
+}
+
+// Decode one symbol from the top `avail` bits of `w` (left-aligned in 32
+// bits).  Returns the symbol and sets *len, or -1 if no code of length
+// <= avail is complete.
+int
+canon_decode(const Canon *c, uint32_t w, int avail, int *len)
+{
+    for (int L = 1; L <= avail && L <= 30; ++L)
+    {
+        uint32_t v = w >> (32 - L);
+        if (c->count[L] && v - c->first[L] < c->count[L])
+        {
+            *len = L;
+            return c->sorted[c->base[L] + (v - c->first[L])];
+        }
+    }
+    return -1;
+}
+
+}  // namespace
+
+void
+build_tables(HostTables *t)
+{
+    Canon c;
+    canon_build(&c, t->code);
+    for (int s = 0; s < 257; ++s)
+        t->bits[s] = kLen[s];
+    memcpy(t->sorted, c.sorted, sizeof(t->sorted));
+
+    for (uint32_t w = 0; w < (uint32_t) kWinSize; ++w)
+    {
+        uint32_t left = w << (32 - kWinBits);
+        int l0, l1;
+        int s0 = canon_decode(&c, left, kWinBits, &l0);
+        uint32_t e = 0;
+        if (s0 >= 0 && s0 < 256)
+        {
+            e = (uint32_t) s0 | ((uint32_t) l0 << 16) | ((uint32_t) l0 << 20)
+              | (1u << 24);
+            int s1 = canon_decode(&c, left << l0, kWinBits - l0, &l1);
+            if (s1 >= 0 && s1 < 256)
+                e = (uint32_t) s0 | ((uint32_t) s1 << 8) | ((uint32_t) l0 << 16)
+                  | ((uint32_t) (l0 + l1) << 20) | (2u << 24);
+        }
+        t->win[w] = e;
+    }
+
+    t->n_long = 0;
+    for (int L = kWinBits + 1; L <= 30; ++L)
+        if (c.count[L])
+        {
+            LongLen &ll = t->longc[t->n_long++];
+            ll.len = (uint32_t) L;
+            ll.first = c.first[L];
+            ll.count = c.count[L];
+            ll.base = c.base[L];
+        }
+}
+
+}  // namespace qhuff

@@ -1,0 +1,253 @@
+"""Python plumbing over libqhuff.so (include/qhuff.h).
+
+The product is the C-ABI library (HIP kernels for gfx950 + host C); this
+module only binds it with ctypes so tests and bench.py can drive it with
+torch device tensors.  There is no CPU fallback: if libqhuff.so is missing or
+no gfx950 device is usable, Codec() raises.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)                 # .../ls-qpack_amd
+LIB_PATH = os.path.join(PKG_ROOT, "libqhuff.so")
+HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "qhuff.h")
+
+OK = 0
+EINVAL, ENOMEM, ENODEV, ERANGE, EDEVICE = -22, -12, -19, -34, -5
+ENC_PAYLOAD, ENC_LITERAL3, ENC_LITERAL5, ENC_LITERAL7 = 0, 3, 5, 7
+DEC_OK, DEC_ERROR = 0, 1
+HUFF_DEC_OK, HUFF_DEC_END_SRC, HUFF_DEC_END_DST, HUFF_DEC_ERROR = 0, 1, 2, 3
+
+# every function include/qhuff.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "qhuff_open", "qhuff_close", "qhuff_encode_bound", "qhuff_decode_bound",
+    "qhuff_encode_batch", "qhuff_decode_batch", "qhuff_encode_batch_host",
+    "qhuff_decode_batch_host", "qhuff_enc_enc_str", "qhuff_enc_str_size",
+    "qhuff_huff_decode", "qhuff_last_error", "qhuff_shard_cuts",
+    "qhuff_synth_batch",
+)
+
+
+class QhuffError(RuntimeError):
+    pass
+
+
+class DecodeRetval(C.Structure):
+    _fields_ = [("status", C.c_int), ("n_dst", C.c_uint), ("n_src", C.c_uint)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libqhuff.so (built by `make -C ls-qpack_amd`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise QhuffError("libqhuff.so not built: run make -C %s" % PKG_ROOT)
+        L = C.CDLL(LIB_PATH)
+        vp, u32p = C.c_void_p, C.c_void_p
+        L.qhuff_open.restype = C.c_int
+        L.qhuff_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.qhuff_close.restype = None
+        L.qhuff_close.argtypes = [vp]
+        L.qhuff_encode_bound.restype = C.c_uint64
+        L.qhuff_encode_bound.argtypes = [C.c_uint64, C.c_uint32, C.c_uint]
+        L.qhuff_decode_bound.restype = C.c_uint64
+        L.qhuff_decode_bound.argtypes = [C.c_uint64, C.c_uint32]
+        L.qhuff_encode_batch.restype = C.c_int
+        L.qhuff_encode_batch.argtypes = [vp, vp, u32p, C.c_uint32, C.c_uint,
+                                         vp, u32p, vp]
+        L.qhuff_decode_batch.restype = C.c_int
+        L.qhuff_decode_batch.argtypes = [vp, vp, u32p, C.c_uint32, vp, u32p,
+                                         vp, vp]
+        L.qhuff_encode_batch_host.restype = C.c_int
+        L.qhuff_encode_batch_host.argtypes = [vp, vp, u32p, C.c_uint32,
+                                              C.c_uint, vp, u32p]
+        L.qhuff_decode_batch_host.restype = C.c_int
+        L.qhuff_decode_batch_host.argtypes = [vp, vp, u32p, C.c_uint32, vp,
+                                              u32p, vp]
+        L.qhuff_enc_enc_str.restype = C.c_int
+        L.qhuff_enc_enc_str.argtypes = [vp, C.c_uint, vp, C.c_size_t,
+                                        C.c_char_p, C.c_uint]
+        L.qhuff_enc_str_size.restype = C.c_uint
+        L.qhuff_enc_str_size.argtypes = [vp, C.c_char_p, C.c_uint]
+        L.qhuff_huff_decode.restype = DecodeRetval
+        L.qhuff_huff_decode.argtypes = [vp, C.c_char_p, C.c_int, vp, C.c_int]
+        L.qhuff_last_error.restype = C.c_char_p
+        L.qhuff_last_error.argtypes = [vp]
+        L.qhuff_shard_cuts.restype = C.c_int
+        L.qhuff_shard_cuts.argtypes = [u32p, C.c_uint32, C.c_uint32, u32p]
+        L.qhuff_synth_batch.restype = C.c_uint64
+        L.qhuff_synth_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32,
+                                        C.c_uint32, C.c_char_p, C.c_uint32,
+                                        vp, u32p]
+        _lib = L
+    return _lib
+
+
+# ---- host-only helpers (no device needed) ---------------------------------
+
+def encode_bound(in_bytes, n, mode=ENC_PAYLOAD):
+    return int(lib().qhuff_encode_bound(in_bytes, n, mode))
+
+
+def decode_bound(in_bytes, n):
+    return int(lib().qhuff_decode_bound(in_bytes, n))
+
+
+def _np_ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def shard_cuts(in_off, g):
+    """Byte-balanced contiguous partition into g shards -> g+1 string
+    indices (include/qhuff.h qhuff_shard_cuts)."""
+    import numpy as np
+    in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
+    cuts = np.zeros(g + 1, dtype=np.uint32)
+    rc = lib().qhuff_shard_cuts(_np_ptr(in_off), len(in_off) - 1, g,
+                                _np_ptr(cuts))
+    if rc:
+        raise QhuffError("qhuff_shard_cuts: %d" % rc)
+    return cuts
+
+
+TOKEN_ALPHABET = b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, "
+BASE64_ALPHABET = (b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz"
+                   b"0123456789+/")
+
+
+def synth_batch(n, seed=0, min_len=8, max_len=64, alphabet=TOKEN_ALPHABET):
+    """Synthetic header strings: returns (data uint8,
+    in_off uint32[n+1]) numpy arrays."""
+    import numpy as np
+    data = np.zeros(max(n * max_len, 1), dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.uint32)
+    tot = lib().qhuff_synth_batch(seed, n, min_len, max_len, alphabet,
+                                  len(alphabet), _np_ptr(data), _np_ptr(off))
+    return data[:tot].copy(), off
+
+
+# ---- device codec ----------------------------------------------------------
+
+class Codec:
+    """One qhuff_ctx on one GPU.  Tensor arguments are torch CUDA(HIP)
+    tensors; offsets are int32 tensors reinterpreted as uint32."""
+
+    def __init__(self, device=0):
+        self._ctx = C.c_void_p()
+        rc = lib().qhuff_open(device, C.byref(self._ctx))
+        if rc != OK:
+            raise QhuffError("qhuff_open(device=%d) failed: %d" % (device, rc))
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            lib().qhuff_close(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != OK:
+            err = lib().qhuff_last_error(self._ctx)
+            raise QhuffError("%s failed: %d (%s)" % (what, rc,
+                             err.decode() if err else ""))
+
+    @staticmethod
+    def _stream(stream):
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream()
+        return C.c_void_p(stream.cuda_stream)
+
+    # device-resident batch calls ------------------------------------------
+    def encode_into(self, data, in_off, n, mode, out, out_off, stream=None):
+        rc = lib().qhuff_encode_batch(self._ctx, data.data_ptr(),
+                                      in_off.data_ptr(), n, mode,
+                                      out.data_ptr(), out_off.data_ptr(),
+                                      self._stream(stream))
+        self._check(rc, "qhuff_encode_batch")
+
+    def decode_into(self, data, in_off, n, out, out_off, status, stream=None):
+        rc = lib().qhuff_decode_batch(self._ctx, data.data_ptr(),
+                                      in_off.data_ptr(), n, out.data_ptr(),
+                                      out_off.data_ptr(), status.data_ptr(),
+                                      self._stream(stream))
+        self._check(rc, "qhuff_decode_batch")
+
+    def encode(self, data, in_off, mode=ENC_PAYLOAD, stream=None):
+        """data: uint8 cuda tensor, in_off: int32 cuda tensor [n+1].
+        Returns (out uint8 [bound], out_off int32 [n+1])."""
+        import torch
+        n = in_off.numel() - 1
+        in_bytes = int(data.numel())
+        out = torch.empty(encode_bound(in_bytes, n, mode), dtype=torch.uint8,
+                          device=data.device)
+        out_off = torch.empty(n + 1, dtype=torch.int32, device=data.device)
+        self.encode_into(data, in_off, n, mode, out, out_off, stream)
+        return out, out_off
+
+    def decode(self, data, in_off, stream=None):
+        import torch
+        n = in_off.numel() - 1
+        out = torch.empty(decode_bound(int(data.numel()), n),
+                          dtype=torch.uint8, device=data.device)
+        out_off = torch.empty(n + 1, dtype=torch.int32, device=data.device)
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=data.device)
+        self.decode_into(data, in_off, n, out, out_off, status, stream)
+        return out, out_off, status[:n]
+
+    # host-memory batch calls (numpy) ----------------------------------------
+    def encode_host(self, data, in_off, mode=ENC_PAYLOAD):
+        import numpy as np
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
+        n = len(in_off) - 1
+        out = np.zeros(encode_bound(int(in_off[-1] - in_off[0]), n, mode),
+                       dtype=np.uint8)
+        out_off = np.zeros(n + 1, dtype=np.uint32)
+        rc = lib().qhuff_encode_batch_host(self._ctx, _np_ptr(data),
+                                           _np_ptr(in_off), n, mode,
+                                           _np_ptr(out), _np_ptr(out_off))
+        self._check(rc, "qhuff_encode_batch_host")
+        return out[:out_off[-1]], out_off
+
+    def decode_host(self, data, in_off):
+        import numpy as np
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
+        n = len(in_off) - 1
+        out = np.zeros(decode_bound(int(in_off[-1] - in_off[0]), n),
+                       dtype=np.uint8)
+        out_off = np.zeros(n + 1, dtype=np.uint32)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        rc = lib().qhuff_decode_batch_host(self._ctx, _np_ptr(data),
+                                           _np_ptr(in_off), n, _np_ptr(out),
+                                           _np_ptr(out_off), _np_ptr(status))
+        self._check(rc, "qhuff_decode_batch_host")
+        return out[:out_off[-1]], out_off, status[:n]
+
+    # per-string mirrors of the reference entry points ----------------------
+    def enc_enc_str(self, prefix_bits, s, first_byte=0, dst_len=1 << 20):
+        buf = C.create_string_buffer(max(dst_len, 1))
+        buf[0] = first_byte
+        r = lib().qhuff_enc_enc_str(self._ctx, prefix_bits, buf, dst_len, s,
+                                    len(s))
+        return r if r < 0 else buf.raw[:r]
+
+    def enc_str_size(self, s):
+        return int(lib().qhuff_enc_str_size(self._ctx, s, len(s)))
+
+    def huff_decode(self, src, dst_len=None):
+        if dst_len is None:
+            dst_len = len(src) * 8 // 5 + 1
+        d = C.create_string_buffer(max(dst_len, 1))
+        rv = lib().qhuff_huff_decode(self._ctx, src, len(src), d, dst_len)
+        return rv.status, d.raw[:rv.n_dst], rv.n_src

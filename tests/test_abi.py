@@ -1,0 +1,108 @@
+"""CPU-side checks of the product boundary: libqhuff.so builds for gfx950,
+loads, exports every entry point include/qhuff.h declares, and its host-only
+helpers behave.  No kernel is launched here (no GPU in the build container)."""
+import ctypes as C
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import _paths  # noqa: F401
+import qhuff
+
+
+def header_functions():
+    text = open(qhuff.HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b(qhuff_\w+)\s*\(", text)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = qhuff.lib()
+    declared = header_functions()
+    assert len(declared) >= 14
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(qhuff.EXPORTS) == declared
+    out = subprocess.check_output(["nm", "-D", "--defined-only",
+                                   qhuff.LIB_PATH]).decode()
+    exported = set(re.findall(r" T (qhuff_\w+)", out))
+    assert set(declared) <= exported
+
+
+def test_library_has_gfx950_code_object():
+    blob = open(qhuff.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_header_is_plain_c():
+    """The boundary header must compile as C99 with no HIP/torch types."""
+    src = '#include "%s"\nint main(void){return QHUFF_ABI_VERSION != 1;}\n' \
+        % qhuff.HEADER
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-x", "c",
+                        "-fsyntax-only", "-"], input=src, text=True,
+                       capture_output=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_open_fails_loudly_without_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    ctx = C.c_void_p()
+    rc = qhuff.lib().qhuff_open(0, C.byref(ctx))
+    assert rc == qhuff.ENODEV and not ctx.value
+    with pytest.raises(qhuff.QhuffError):
+        qhuff.Codec(0)
+
+
+def test_bounds():
+    assert qhuff.decode_bound(5, 1) >= 8
+    for n in (1, 10, 1000):
+        # 30-bit code per byte
+        assert qhuff.encode_bound(64 * n, n, 0) >= (64 * n * 30 + 7) // 8
+        assert qhuff.encode_bound(64 * n, n, 7) >= qhuff.encode_bound(64 * n, n, 0)
+
+
+def xorshift(x):
+    x ^= (x << 13) & 0xFFFFFFFFFFFFFFFF
+    x ^= x >> 7
+    x ^= (x << 17) & 0xFFFFFFFFFFFFFFFF
+    return x
+
+
+def test_synth_batch_matches_generator_spec():
+    """xorshift64, seed 0x9E3779B97F4A7C15, len = 8 + r % 57,
+    bytes alphabet[r % |alphabet|]."""
+    data, off = qhuff.synth_batch(200)
+    x = 0x9E3779B97F4A7C15
+    a = qhuff.TOKEN_ALPHABET
+    pos = 0
+    for i in range(200):
+        x = xorshift(x)
+        ln = 8 + x % 57
+        assert off[i] == pos and off[i + 1] - off[i] == ln
+        for k in range(ln):
+            x = xorshift(x)
+            assert data[pos] == a[x % len(a)]
+            pos += 1
+    assert off[200] == pos == len(data)
+
+
+def test_shard_cuts_balance():
+    data, off = qhuff.synth_batch(10000, seed=3)
+    for g in (1, 2, 3, 4, 8):
+        cuts = qhuff.shard_cuts(off, g)
+        assert cuts[0] == 0 and cuts[-1] == 10000
+        assert np.all(np.diff(cuts.astype(np.int64)) >= 0)
+        sizes = [int(off[cuts[k + 1]]) - int(off[cuts[k]]) for k in range(g)]
+        assert sum(sizes) == len(data)
+        assert max(sizes) - min(sizes) <= 2 * 64
+    # degenerate: more shards than strings, empty batch
+    off3 = np.array([0, 5, 9, 20], dtype=np.uint32)
+    cuts = qhuff.shard_cuts(off3, 8)
+    assert cuts[0] == 0 and cuts[-1] == 3 and np.all(np.diff(cuts.astype(int)) >= 0)
+    cuts = qhuff.shard_cuts(np.array([0], dtype=np.uint32), 4)
+    assert list(cuts) == [0, 0, 0, 0, 0]

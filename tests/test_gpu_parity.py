@@ -1,0 +1,294 @@
+"""GPU parity: the HIP path through the C-ABI (libqhuff.so) against the CPU
+oracle and the reference's own golden vectors.  Bit-exact everywhere (this
+is byte/integer work): output bytes, out_off, and per-string status."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import _paths  # noqa: F401
+import oracle_lib as O
+import qpack_frames as Q
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import qhuff
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test without a GPU")
+    c = qhuff.Codec(0)
+    yield c
+    c.close()
+
+
+def pack(strings):
+    off = np.zeros(len(strings) + 1, dtype=np.uint32)
+    np.cumsum([len(s) for s in strings], out=off[1:])
+    data = np.frombuffer(b"".join(strings), dtype=np.uint8).copy()
+    return data, off
+
+
+def to_dev(data, off, pad_front=0):
+    """Device copies; pad_front shifts the data pointer off 16-byte alignment
+    and in_off[0] away from 0 (both allowed by the ABI)."""
+    d = torch.zeros(len(data) + pad_front + 16, dtype=torch.uint8,
+                    device="cuda")
+    if len(data):
+        d[pad_front:pad_front + len(data)] = torch.from_numpy(data).cuda()
+    o = torch.from_numpy(off.astype(np.int64) + pad_front).to(torch.int32).cuda()
+    return d, o
+
+
+def gpu_encode(codec, data, off, mode=0, pad_front=0):
+    d, o = to_dev(data, off, pad_front)
+    out, out_off = codec.encode(d, o, mode)
+    torch.cuda.synchronize()
+    oo = out_off.cpu().numpy().view(np.uint32)
+    return out[:int(oo[-1])].cpu().numpy(), oo
+
+
+def gpu_decode(codec, data, off, pad_front=0):
+    d, o = to_dev(data, off, pad_front)
+    out, out_off, status = codec.decode(d, o)
+    torch.cuda.synchronize()
+    oo = out_off.cpu().numpy().view(np.uint32)
+    return out[:int(oo[-1])].cpu().numpy(), oo, status.cpu().numpy()
+
+
+def check_encode(codec, data, off, mode, pad_front=0):
+    g_out, g_off = gpu_encode(codec, data, off, mode, pad_front)
+    o_out, o_off = O.encode_batch(data, off, mode)
+    assert np.array_equal(g_off, o_off)
+    assert np.array_equal(g_out, o_out)
+    return g_out, g_off
+
+
+def check_decode(codec, data, off, pad_front=0):
+    g_out, g_off, g_st = gpu_decode(codec, data, off, pad_front)
+    o_out, o_off, o_st = O.decode_batch(data, off)
+    assert np.array_equal(g_st, o_st)
+    assert np.array_equal(g_off, o_off)
+    assert np.array_equal(g_out, o_out)
+    return g_out, g_off, g_st
+
+
+def load(name):
+    with open(os.path.join(G, name)) as f:
+        return json.load(f)
+
+
+# ---- golden vectors ------------------------------------------------------------
+
+def test_decode_kats(codec):
+    kat = load("kat_huff_decode.json")
+    ok = [bytes.fromhex(k["huff"]) for k in kat["decode_ok"]]
+    bad = [bytes.fromhex(k["huff"]) for k in kat["decode_error"]]
+    data, off = pack(ok + bad)
+    out, oo, st = gpu_decode(codec, data, off)
+    for i, k in enumerate(kat["decode_ok"]):
+        assert st[i] == 0
+        assert bytes(out[oo[i]:oo[i + 1]]) == bytes.fromhex(k["plain"])
+    assert list(st[len(ok):]) == [1] * len(bad)
+    check_decode(codec, data, off)
+
+
+def test_encode_kats(codec):
+    kat = load("kat_huff_decode.json")["decode_ok"]
+    data, off = pack([bytes.fromhex(k["plain"]) for k in kat])
+    out, oo = check_encode(codec, data, off, 0)
+    for i, k in enumerate(kat):
+        assert bytes(out[oo[i]:oo[i + 1]]) == bytes.fromhex(k["huff"])
+
+
+def test_enc_str_kats(codec):
+    kat = load("kat_enc_str.json")["enc_str"]
+    assert all(k["prefix_bits"] == 3 for k in kat)
+    data, off = pack([bytes.fromhex(k["str"]) for k in kat])
+    out, oo = check_encode(codec, data, off, 3)
+    for i, k in enumerate(kat):
+        assert bytes(out[oo[i]:oo[i + 1]]) == bytes.fromhex(k["out"])
+        assert oo[i + 1] - oo[i] == k["retval"]
+
+
+@pytest.mark.parametrize("corpus", ["netbsd", "fb-req", "fb-resp"])
+def test_reference_encoded_stream_literals(codec, corpus):
+    """Every literal of the reference-encoded interop stream: the GPU decodes
+    the Huffman payloads, and re-encodes the strings with the same framing
+    bit for bit (prefix 3/5/7 batches)."""
+    raw = open(os.path.join(G, "data", corpus + ".out.256.100.1"), "rb").read()
+    lits = Q.stream_literals(raw)
+    huff = [l for l in lits if l["huffman"]]
+    data, off = pack([l["payload"] for l in huff])
+    out, oo, st = check_decode(codec, data, off)
+    assert not st.any()
+    plain = {id(l): bytes(out[oo[i]:oo[i + 1]]) for i, l in enumerate(huff)}
+    for p in (3, 5, 7):
+        sel = [l for l in lits if l["prefix_bits"] == p]
+        if not sel:
+            continue
+        strs = [plain[id(l)] if l["huffman"] else l["payload"] for l in sel]
+        d2, o2 = pack(strs)
+        e, eo = check_encode(codec, d2, o2, p)
+        for i, l in enumerate(sel):
+            wire = bytearray(e[eo[i]:eo[i + 1]])
+            hib = l["first_byte"] & ~((1 << (p + 1)) - 1) & 0xFF
+            wire[0] |= hib
+            assert bytes(wire) == l["wire"]
+
+
+def test_qif_corpus_round_trip(codec):
+    """All names and values of the four QIF corpora (real header strings,
+    incl. long-codes.qif): encode in every mode, decode the payloads."""
+    strs = []
+    for fn in ("netbsd.qif", "fb-req.qif", "fb-resp.qif", "long-codes.qif"):
+        for hl in Q.qif_header_lists(open(os.path.join(G, "data", fn), "rb").read()):
+            for n, v in hl:
+                strs += [n, v]
+    data, off = pack(strs)
+    for mode in (0, 3, 5, 7):
+        check_encode(codec, data, off, mode)
+    h, ho = check_encode(codec, data, off, 0)
+    out, oo, st = check_decode(codec, h, ho)
+    assert not st.any()
+    assert np.array_equal(out, data) and np.array_equal(oo, off - off[0])
+
+
+# ---- synthetic + adversarial batches -----------------------------------------------
+
+def rand_strings(rng, n, alpha, lo, hi):
+    return [bytes(rng.choice(alpha) for _ in range(rng.randint(lo, hi)))
+            for _ in range(n)]
+
+
+ALPHAS = {
+    "token": b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, ",
+    "all": bytes(range(256)),
+    "long": b"\x01\x02\x06\x5c\x8d" + b"abcdefgh",
+    "high": bytes(range(128, 256)),
+}
+
+
+@pytest.mark.parametrize("alpha", sorted(ALPHAS))
+@pytest.mark.parametrize("mode", [0, 3, 5, 7])
+def test_encode_random(codec, alpha, mode):
+    rng = random.Random(hash((alpha, mode)) & 0xffff)
+    strs = rand_strings(rng, 3000, ALPHAS[alpha], 0, 80)
+    data, off = pack(strs)
+    check_encode(codec, data, off, mode)
+    check_encode(codec, data, off, mode, pad_front=5)
+
+
+@pytest.mark.parametrize("alpha", sorted(ALPHAS))
+def test_decode_random_valid(codec, alpha):
+    rng = random.Random(len(alpha))
+    strs = rand_strings(rng, 3000, ALPHAS[alpha], 0, 80)
+    data, off = pack(strs)
+    h, ho = O.encode_batch(data, off, 0)
+    out, oo, st = check_decode(codec, h, ho)
+    assert not st.any() and np.array_equal(out, data)
+    check_decode(codec, h, ho, pad_front=3)
+
+
+def test_decode_garbage(codec):
+    """Random bytes: mostly rejects (EOS, long padding, non-ones padding);
+    accept/reject and output must match the reference decoder exactly."""
+    rng = random.Random(11)
+    strs = [bytes(rng.randrange(256) for _ in range(rng.randint(0, 40)))
+            for _ in range(20000)]
+    # near-valid: valid encodings with the last byte perturbed / extended
+    for i in range(5000):
+        s = rand_strings(rng, 1, ALPHAS["token"], 1, 30)[0]
+        h = bytearray(O.huffman_enc(s))
+        r = i % 4
+        if r == 0:
+            h[-1] ^= 1 << rng.randrange(8)
+        elif r == 1:
+            h += b"\xff"
+        elif r == 2:
+            h += bytes([rng.randrange(256)])
+        else:
+            h = h[:-1]
+        strs.append(bytes(h))
+    # EOS and long ones runs embedded
+    strs += [b"\xff\xff\xff\xfc", b"\xff\xff\xff\xff", b"\x00\xff\xff\xff\xff",
+             b"\xfe\xff\xff\xff\xff\x80", b"\x1f\xff", b"\x1f\xff\xff",
+             b"\x7f", b"\x3f", b"\x0f\xff"]
+    data, off = pack(strs)
+    out, oo, st = check_decode(codec, data, off)
+    assert st.sum() > 1000 and (st == 0).sum() > 1000
+
+
+def test_edge_batches(codec):
+    # n = 0
+    for mode in (0, 7):
+        out, oo = gpu_encode(codec, np.zeros(0, np.uint8),
+                             np.zeros(1, np.uint32), mode)
+        assert list(oo) == [0]
+    # all-empty strings, single string, one huge string (direct paths)
+    check_encode(codec, *pack([b""] * 1000), 0)
+    check_encode(codec, *pack([b""] * 1000), 7)
+    check_decode(codec, *pack([b""] * 1000))
+    rng = random.Random(5)
+    big = bytes(rng.choice(ALPHAS["all"]) for _ in range(70000))
+    for strs in ([b"x"], [big], [b"ab"] * 300 + [big] + [b"cd"] * 300):
+        data, off = pack(strs)
+        for mode in (0, 3, 7):
+            check_encode(codec, data, off, mode)
+        h, ho = O.encode_batch(data, off, 0)
+        out, oo, st = check_decode(codec, h, ho)
+        assert np.array_equal(out, data)
+    # strings whose decode output overflows the LDS slot (96 B) and tiles whose
+    # input overflows the LDS stage
+    strs = rand_strings(rng, 600, ALPHAS["token"], 90, 300)
+    data, off = pack(strs)
+    check_encode(codec, data, off, 0)
+    h, ho = O.encode_batch(data, off, 0)
+    check_decode(codec, h, ho)
+
+
+def test_full_size_round_trip(codec):
+    """BASELINE config 2/3 size (1M strings, U[8,64] token alphabet): GPU
+    sizes and bytes equal the oracle's; decode(encode(x)) == x."""
+    import qhuff
+    data, off = qhuff.synth_batch(1 << 20)
+    g_out, g_off = check_encode(codec, data, off, 0)
+    out, oo, st = check_decode(codec, g_out, g_off)
+    assert not st.any()
+    assert np.array_equal(out, data) and np.array_equal(oo, off)
+    check_encode(codec, data, off, 7)
+
+
+def test_host_path_and_mirrors(codec):
+    rng = random.Random(9)
+    strs = rand_strings(rng, 500, ALPHAS["all"], 0, 50)
+    data, off = pack(strs)
+    for mode in (0, 5):
+        e, eo = codec.encode_host(data, off, mode)
+        o, oo2 = O.encode_batch(data, off, mode)
+        assert np.array_equal(e, o) and np.array_equal(eo, oo2)
+    h, ho = O.encode_batch(data, off, 0)
+    d, do, st = codec.decode_host(h, ho)
+    assert not st.any() and np.array_equal(d, data)
+    # per-string mirrors of lsqpack_enc_enc_str / qenc_enc_str_size /
+    # lsqpack_huff_decode
+    for k in load("kat_enc_str.json")["enc_str"]:
+        s = bytes.fromhex(k["str"])
+        assert codec.enc_enc_str(3, s, dst_len=0x1000) == bytes.fromhex(k["out"])
+    assert codec.enc_enc_str(3, b"aaa", dst_len=2) == -1
+    r = codec.enc_enc_str(5, b"www.netbsd.org", first_byte=0xC0)
+    assert r == O.enc_enc_str(5, b"www.netbsd.org", first_byte=0xC0)
+    assert codec.enc_str_size(b"www.netbsd.org") == 11
+    st, out, n_src = codec.huff_decode(bytes.fromhex("f1e3c2f51531a245cf64df"))
+    assert st == 0 and out == b"www.netbsd.org" and n_src == 11
+    st, out, _ = codec.huff_decode(b"\xff")
+    assert st == 3
+    st, out, _ = codec.huff_decode(bytes.fromhex("f1e3c2f51531a245cf64df"),
+                                   dst_len=4)
+    assert st == 2
