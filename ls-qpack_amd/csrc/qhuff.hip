@@ -34,7 +34,14 @@ namespace qhuff {
 constexpr int kTile = 256;                 // strings per tile = threads per WG
 constexpr int kEncInCap = 16 * 1024;       // staged input bytes per encode tile
 constexpr int kDecInCap = 12 * 1024;       // staged input bytes per decode tile
-constexpr int kSlot = 96;                  // LDS output slot per decode lane
+constexpr int kSlot = 100;                 // LDS output slot per decode lane
+                                           // (25 dwords: odd stride, no bank conflicts)
+
+// ablation switches (timing experiments only; outputs are wrong when set)
+constexpr uint32_t kDbgNoTicket = 1;       // tile = blockIdx.x
+constexpr uint32_t kDbgNoLookback = 2;     // base = tile * 64 KiB
+constexpr uint32_t kDbgNoStore = 4;        // skip output stores
+constexpr uint32_t kDbgNoCodec = 8;        // skip the per-string codec loop
 
 // look-back flag word: [63:62] state, [61:40] epoch, [39:0] inclusive or
 // aggregate byte count
@@ -73,16 +80,22 @@ align_bytes(uint32_t hi, uint32_t lo, uint32_t sh)
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
+// explicit address spaces: a generic pointer into LDS would compile to
+// flat_load (global-memory latency) instead of ds_read
+#define QH_LDS __attribute__((address_space(3)))
+#define QH_GLB __attribute__((address_space(1)))
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 // uniform-per-launch source of aligned input dwords: LDS stage or global
 struct LdsSrc
 {
-    const uint32_t *w;
+    const QH_LDS uint32_t *w;
     __device__ __forceinline__ uint32_t dw(uint32_t i) const { return w[i]; }
 };
 
 struct GlobalSrc
 {
-    const uint32_t *w;
+    const QH_GLB uint32_t *w;
     __device__ __forceinline__ uint32_t dw(uint32_t i) const { return w[i]; }
 };
 
@@ -236,6 +249,7 @@ struct EncArgs
     uint32_t n;
     uint32_t epoch;
     uint32_t mode;            // 0 payload, 3/5/7 literal prefix bits
+    uint32_t dbg;             // ablation switches (QHUFF_DEBUG), 0 in use
 };
 
 // number of bytes of an HPACK prefixed integer (lsqpack_val2len,
@@ -315,7 +329,8 @@ enc_tile_body(const EncArgs &a, const Src &src, uint32_t s, bool valid,
     bool huff = true;
     if (valid)
     {
-        uint32_t hb = (enc_bits(src, rs, re, s_bits) + 7) >> 3;
+        uint32_t hb = (a.dbg & kDbgNoCodec) ? len
+                    : (enc_bits(src, rs, re, s_bits) + 7) >> 3;
         if (a.mode == 0)
             size = hb;
         else
@@ -334,14 +349,15 @@ enc_tile_body(const EncArgs &a, const Src &src, uint32_t s, bool valid,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < 64)
     {
-        uint64_t base = look_back(a.flags, tile, total, a.epoch);
+        uint64_t base = (a.dbg & kDbgNoLookback) ? (uint64_t) tile << 16
+                      : look_back(a.flags, tile, total, a.epoch);
         if (tid == 0)
             *s_base = base;
     }
     __syncthreads();
     const uint64_t base = *s_base;
 
-    if (valid)
+    if (valid && !(a.dbg & kDbgNoStore))
     {
         a.out_off[s] = (uint32_t) (base + excl);
         if (s == a.n - 1)
@@ -384,7 +400,8 @@ qhuff_encode_tile(EncArgs a)
 
     const int tid = threadIdx.x;
     if (tid == 0)
-        s_tile = (uint32_t) (atomicAdd(a.ticket, 1ull) - a.ticket_base);
+        s_tile = (a.dbg & kDbgNoTicket) ? blockIdx.x
+               : (uint32_t) (atomicAdd(a.ticket, 1ull) - a.ticket_base);
     s_enc[tid] = a.tab->enc[tid];
     s_bits[tid] = (uint8_t) a.tab->enc[tid].y;
     if (tid == 0)
@@ -408,18 +425,19 @@ qhuff_encode_tile(EncArgs a)
 
     if (pb - pa <= (uintptr_t) kEncInCap)
     {
-        const uint4 *g = (const uint4 *) pa;
+        const QH_GLB u32x4 *g = (const QH_GLB u32x4 *) pa;
+        QH_LDS u32x4 *d4 = (QH_LDS u32x4 *) s_in;
         const uint32_t n16 = (uint32_t) ((pb - pa) >> 4);
         for (uint32_t i = tid; i < n16; i += kTile)
-            s_in[i] = g[i];
+            d4[i] = g[i];
         __syncthreads();
-        LdsSrc src{(const uint32_t *) s_in};
+        LdsSrc src{(const QH_LDS uint32_t *) s_in};
         enc_tile_body(a, src, s, valid, rs, re, s_enc, s_bits, s_wsum,
                       &s_base, tile);
     }
     else
     {
-        GlobalSrc src{(const uint32_t *) pa};
+        GlobalSrc src{(const QH_GLB uint32_t *) pa};
         enc_tile_body(a, src, s, valid, rs, re, s_enc, s_bits, s_wsum,
                       &s_base, tile);
     }
@@ -441,6 +459,7 @@ struct DecArgs
     unsigned long long ticket_base;
     uint32_t n;
     uint32_t epoch;
+    uint32_t dbg;
     LongParams lp;
 };
 
@@ -610,7 +629,9 @@ dec_tile_body(const DecArgs &a, const Src &src, uint32_t s, bool valid,
     uint32_t *slot = s_slots + tid * (kSlot / 4);
     uint32_t nout = 0;
     bool ok = true, over = false;
-    if (valid)
+    if (valid && (a.dbg & kDbgNoCodec))
+        nout = re - rs;
+    else if (valid)
     {
         SlotSink sink;
         sink.init(slot, kSlot / 4);
@@ -626,13 +647,14 @@ dec_tile_body(const DecArgs &a, const Src &src, uint32_t s, bool valid,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < 64)
     {
-        uint64_t base = look_back(a.flags, tile, total, a.epoch);
+        uint64_t base = (a.dbg & kDbgNoLookback) ? (uint64_t) tile << 16
+                      : look_back(a.flags, tile, total, a.epoch);
         if (tid == 0)
             *s_base = base;
     }
     __syncthreads();
     const uint64_t base = *s_base;
-    if (!valid)
+    if (!valid || (a.dbg & kDbgNoStore))
         return;
     a.out_off[s] = (uint32_t) (base + excl);
     a.status[s] = ok ? QHUFF_DEC_OK : QHUFF_DEC_ERROR;
@@ -680,7 +702,8 @@ qhuff_decode_tile(DecArgs a)
 
     const int tid = threadIdx.x;
     if (tid == 0)
-        s_tile = (uint32_t) (atomicAdd(a.ticket, 1ull) - a.ticket_base);
+        s_tile = (a.dbg & kDbgNoTicket) ? blockIdx.x
+               : (uint32_t) (atomicAdd(a.ticket, 1ull) - a.ticket_base);
     {
         const uint4 *gw = (const uint4 *) a.tab->win;
         uint4 *sw = (uint4 *) s_win;
@@ -708,18 +731,19 @@ qhuff_decode_tile(DecArgs a)
     }
     if (pb - pa <= (uintptr_t) kDecInCap)
     {
-        const uint4 *g = (const uint4 *) pa;
+        const QH_GLB u32x4 *g = (const QH_GLB u32x4 *) pa;
+        QH_LDS u32x4 *d4 = (QH_LDS u32x4 *) s_in;
         const uint32_t n16 = (uint32_t) ((pb - pa) >> 4);
         for (uint32_t i = tid; i < n16; i += kTile)
-            s_in[i] = g[i];
+            d4[i] = g[i];
         __syncthreads();
-        LdsSrc src{(const uint32_t *) s_in};
+        LdsSrc src{(const QH_LDS uint32_t *) s_in};
         dec_tile_body(a, src, s, valid, rs, re, s_win, s_sorted, s_slots,
                       s_wsum, &s_base, tile);
     }
     else
     {
-        GlobalSrc src{(const uint32_t *) pa};
+        GlobalSrc src{(const QH_GLB uint32_t *) pa};
         dec_tile_body(a, src, s, valid, rs, re, s_win, s_sorted, s_slots,
                       s_wsum, &s_base, tile);
     }
@@ -743,6 +767,7 @@ struct qhuff_ctx
     uint64_t cap_tiles;
     unsigned long long ticket_base;
     uint32_t epoch;
+    uint32_t dbg;                        // QHUFF_DEBUG ablation switches
     // host-path staging
     uint8_t *h_stage;                    // pinned
     size_t h_stage_cap;
@@ -818,6 +843,10 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         return rc;
     }
     c->epoch = 0;
+    {
+        const char *d = getenv("QHUFF_DEBUG");
+        c->dbg = d ? (uint32_t) strtoul(d, nullptr, 0) : 0;
+    }
     *ctx_out = c;
     return QHUFF_OK;
 }
@@ -929,6 +958,7 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.n = n;
     a.epoch = c->epoch;
     a.mode = mode;
+    a.dbg = c->dbg;
     hipLaunchKernelGGL(qhuff_encode_tile, dim3((uint32_t) tiles), dim3(kTile),
                        0, st, a);
     HIPCHK(c, hipGetLastError());
@@ -966,6 +996,7 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.ticket_base = c->ticket_base;
     a.n = n;
     a.epoch = c->epoch;
+    a.dbg = c->dbg;
     a.lp = c->lp;
     hipLaunchKernelGGL(qhuff_decode_tile, dim3((uint32_t) tiles), dim3(kTile),
                        0, st, a);
