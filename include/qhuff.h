@@ -154,6 +154,12 @@ qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, int src_len,
 /* Last HIP error string for this context (diagnostics). */
 const char *qhuff_last_error(qhuff_ctx *ctx);
 
+/* Synchronise the device and return (then clear) the context's sticky device
+ * error word: 0 = no error; QHUFF_DEVERR_SPIN = a look-back wait gave up
+ * (outputs of that launch are invalid).  Negative QHUFF_E* on HIP failure. */
+#define QHUFF_DEVERR_SPIN 1
+int qhuff_device_error(qhuff_ctx *ctx);
+
 /* ---- multi-GPU sharding helpers (host arithmetic only) ----------------
  * Byte-balanced contiguous partition of a batch into g shards: writes
  * g + 1 string indices to cuts (cuts[0] = 0, cuts[g] = n) so shard k holds

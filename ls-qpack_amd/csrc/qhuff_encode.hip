@@ -1,0 +1,447 @@
+// qhuff_encode.hip -- batch Huffman encode kernel (gfx950).
+//
+// Reference path:
+//   E1 qenc_enc_str_size   lsqpack.c:5198-5210  -> sizing pass below
+//   E2 qenc_huffman_enc    lsqpack.c:5085-5195  -> packing pass below
+//   E3 lsqpack_enc_enc_str lsqpack.c:839-876    -> LITERAL modes (H bit,
+//                          prefixed length, strict-< Huffman-vs-raw choice)
+//
+// Persistent grid: every workgroup is resident and walks tiles t = blockIdx.x,
+// blockIdx.x + gridDim.x, ... (no ticket atomic).  Per tile of 256 strings:
+//   1. stage the tile's packed input bytes into LDS (coalesced 16-B loads);
+//   2. counting-sort the strings by length so each wave runs similar lengths;
+//   3. sizing pass per lane (code-length sum out of an LDS table);
+//   4. workgroup scan -> tile-local output offsets; publish the aggregate;
+//   5. packing pass per lane into a zeroed LDS output stage (MSB-first bit
+//      accumulator, big-endian words OR-ed in, EOS-prefix padding);
+//   6. look-back for the tile's global output base (its latency overlaps the
+//      packing of step 5 in the other resident workgroups);
+//   7. shifted copy-out with 16-byte aligned global stores; out_off stores.
+// Tiles whose input or output does not fit the LDS stages take the same steps
+// with global reads / per-lane global writes (correct, slower).
+#include "qhuff_kernels.h"
+
+namespace qhuff {
+
+constexpr int kEncInCap = 16 * 1024;        // staged input bytes per tile
+constexpr int kEncOutCap = 16 * 1024;       // staged output bytes per tile
+
+// source of aligned input dwords: LDS stage or global
+struct EncLds
+{
+    const QH_LDS uint32_t *w;
+    __device__ __forceinline__ uint32_t dw(uint32_t i) const { return w[i]; }
+};
+struct EncGlb
+{
+    const QH_GLB uint32_t *w;
+    __device__ __forceinline__ uint32_t dw(uint32_t i) const { return w[i]; }
+};
+
+// MSB-first bit packer.  Words are flushed as big-endian dwords at 4-byte
+// aligned positions; `lo`..`hi` are the bytes this string owns.
+struct PackLds                               // OR into a zeroed LDS stage
+{
+    QH_LDS uint32_t *stage;
+    __device__ __forceinline__ void word(uint32_t wpos, uint32_t be,
+                                         uint32_t, uint32_t) const
+    {
+        __hip_atomic_fetch_or(&stage[wpos >> 2], bswap32(be),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+};
+
+struct PackGlb                               // direct global stores
+{
+    uint8_t *out;                            // 4-byte aligned
+    __device__ __forceinline__ void word(uint32_t wpos, uint32_t be,
+                                         uint32_t lo, uint32_t hi) const
+    {
+        if (wpos >= lo && wpos + 4 <= hi)
+            *(QH_GLB uint32_t *) (out + wpos) = bswap32(be);
+        else
+            for (int k = 0; k < 4; ++k)
+            {
+                uint32_t p = wpos + k;
+                if (p >= lo && p < hi)
+                    out[p] = (uint8_t) (be >> (24 - 8 * k));
+            }
+    }
+};
+
+template <class Sink>
+struct Packer
+{
+    Sink sink;
+    uint64_t acc;          // pending bits, left-aligned
+    uint32_t nbits;        // bits in acc, counting the lead-in bytes
+    uint32_t wpos, lo, hi;
+
+    __device__ __forceinline__ void init(uint32_t start, uint32_t end)
+    {
+        lo = start;
+        hi = end;
+        wpos = start & ~3u;
+        nbits = 8u * (start & 3);
+        acc = 0;
+    }
+    __device__ __forceinline__ void put(uint32_t code, uint32_t len)
+    {
+        acc |= (uint64_t) code << (64 - nbits - len);
+        nbits += len;
+        if (nbits >= 32)
+        {
+            sink.word(wpos, (uint32_t) (acc >> 32), lo, hi);
+            acc <<= 32;
+            nbits -= 32;
+            wpos += 4;
+        }
+    }
+    // EOS-prefix padding to a byte boundary, then flush (lsqpack.c:5171-5189)
+    __device__ __forceinline__ void finish()
+    {
+        uint32_t pad = (8 - (nbits & 7)) & 7;
+        acc |= (uint64_t) ((1u << pad) - 1) << (64 - nbits - pad);
+        nbits += pad;
+        while (nbits > 0)
+        {
+            sink.word(wpos, (uint32_t) (acc >> 32), lo, hi);
+            acc <<= 32;
+            nbits = nbits > 32 ? nbits - 32 : 0;
+            wpos += 4;
+        }
+    }
+};
+
+// HPACK prefixed-integer byte count (lsqpack_val2len, lsqpack.c:767-783)
+__device__ __forceinline__ uint32_t
+int_len(uint32_t v, uint32_t prefix)
+{
+    uint32_t mask = (1u << prefix) - 1;
+    if (v < mask)
+        return 1;
+    v -= mask;
+    uint32_t n = 2;
+    while (v >= 128)
+    {
+        v >>= 7;
+        ++n;
+    }
+    return n;
+}
+
+// sum of code lengths over bytes [rs, re) (positions relative to the source)
+template <class Src>
+__device__ __forceinline__ uint32_t
+code_bits(const Src &src, uint32_t rs, uint32_t re, const QH_LDS uint8_t *s_len)
+{
+    uint32_t bits = 0;
+    const uint32_t d0 = rs >> 2, d1 = (re + 3) >> 2;
+    for (uint32_t d = d0; d < d1; ++d)
+    {
+        uint32_t w = src.dw(d);
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+        {
+            uint32_t p = 4 * d + b;
+            uint32_t l = s_len[(w >> (8 * b)) & 0xff];
+            bits += (p >= rs && p < re) ? l : 0;
+        }
+    }
+    return bits;
+}
+
+template <class Src, class Sink>
+__device__ __forceinline__ void
+pack_string(const Src &src, uint32_t rs, uint32_t re, bool raw,
+            const QH_LDS u32x2 *s_enc, Packer<Sink> &pk)
+{
+    const uint32_t d0 = rs >> 2, d1 = (re + 3) >> 2;
+    for (uint32_t d = d0; d < d1; ++d)
+    {
+        uint32_t w = src.dw(d);
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+        {
+            uint32_t p = 4 * d + b;
+            if (p >= rs && p < re)
+            {
+                uint32_t c = (w >> (8 * b)) & 0xff;
+                if (raw)
+                    pk.put(c, 8);
+                else
+                {
+                    u32x2 e = s_enc[c];
+                    pk.put(e.x, e.y);
+                }
+            }
+        }
+    }
+}
+
+// literal framing (lsqpack.c:852-854, 862-864, 819-836): H bit + prefixed
+// length, then the payload
+template <class Src, class Sink>
+__device__ __forceinline__ void
+emit_string(const Src &src, uint32_t rs, uint32_t re, uint32_t mode,
+            bool huff, uint32_t plen, const QH_LDS u32x2 *s_enc,
+            Packer<Sink> &pk)
+{
+    if (mode)
+    {
+        uint32_t mask = (1u << mode) - 1, first = huff ? (1u << mode) : 0;
+        if (plen < mask)
+            pk.put(first | plen, 8);
+        else
+        {
+            pk.put(first | mask, 8);
+            uint32_t v = plen - mask;
+            while (v >= 128)
+            {
+                pk.put(0x80 | (v & 0x7f), 8);
+                v >>= 7;
+            }
+            pk.put(v, 8);
+        }
+    }
+    pack_string(src, rs, re, !huff, s_enc, pk);
+    pk.finish();
+}
+
+struct EncSmem
+{
+    u32x2 enc[257];
+    uint8_t len[256];
+    uint32_t off[2][kTile + 1];      // current / next tile offsets
+    uint32_t size[kTile];
+    uint32_t excl[kTile];
+    uint32_t cnt[kBuckets];
+    uint16_t perm[kTile];
+    LdsScratch scr;
+    alignas(16) uint32_t in[kEncInCap / 4 + 4];
+    alignas(16) uint32_t out[(kEncOutCap + 64) / 4];   // 16 B pad in front
+};
+
+constexpr int kEncChunks = kEncInCap / 16 / kTile;      // prefetch regs
+
+// per-string sizing result
+struct EncSize
+{
+    uint32_t size, plen;
+    bool huff;
+};
+
+template <class Src>
+__device__ __forceinline__ EncSize
+size_string(const EncArgs &a, const Src &src, uint32_t rs, uint32_t re,
+            const QH_LDS uint8_t *s_len)
+{
+    EncSize z;
+    const uint32_t len = re - rs;
+    const uint32_t hb = (a.c.dbg & kDbgNoCodec) ? len
+                      : (code_bits(src, rs, re, s_len) + 7) >> 3;
+    z.huff = true;
+    z.plen = 0;
+    if (a.mode == 0)
+        z.size = hb;
+    else
+    {
+        z.huff = hb < len;                       // strict <, lsqpack.c:848
+        z.plen = z.huff ? hb : len;
+        z.size = int_len(z.plen, a.mode) + z.plen;
+    }
+    return z;
+}
+
+__global__ __launch_bounds__(kTile) void
+qhuff_encode_kernel(EncArgs a)
+{
+    __shared__ EncSmem smem;
+    QH_LDS EncSmem *sm = (QH_LDS EncSmem *) &smem;
+    const int tid = threadIdx.x;
+
+    const QH_GLB u32x2 *genc = (const QH_GLB u32x2 *) a.enc;
+    const u32x2 e_t = genc[tid];
+    sm->enc[tid] = e_t;
+    sm->len[tid] = (uint8_t) e_t.y;
+    if (tid == 0)
+        sm->enc[256] = genc[256];
+
+    const QH_GLB uint32_t *gin_off = glb(a.in_off);
+    const uint32_t G = gridDim.x;
+    uint32_t tile = blockIdx.x;
+    if (tile >= a.c.n_tiles)
+        return;
+
+    // prologue: offsets + input of the first tile
+    Prefetch<kEncChunks> pf;
+    uint32_t cnt = (uint32_t) min((uint64_t) kTile, a.n - (uint64_t) tile * kTile);
+    pf.load_offsets(gin_off, (uint64_t) tile * kTile, cnt);
+    pf.store_offsets(sm->off[0], cnt);
+    __syncthreads();
+    Span sp0 = tile_span(a.in, sm->off[0], cnt, kEncInCap);
+    uintptr_t sp_pa = sp0.pa;
+    uint32_t sp_n16 = sp0.n16;
+    uint32_t sp_staged = sp0.staged;
+    if (sp_staged)
+    {
+        pf.load_chunks(sp_pa, sp_n16);
+        pf.store_chunks<false>((QH_LDS u32x4 *) sm->in, sp_n16);
+    }
+    uint32_t cur = 0;
+    int64_t known_tile = -1;                      // see look_back()
+    uint64_t known_incl = 0;
+
+    for (;;)
+    {
+        const QH_LDS uint32_t *off = sm->off[cur];
+        const uint64_t s0 = (uint64_t) tile * kTile;
+        const uint32_t next = tile + G;
+        const bool has_next = next < a.c.n_tiles;
+        const uint32_t cnt_n = has_next
+            ? (uint32_t) min((uint64_t) kTile, a.n - (uint64_t) next * kTile) : 0;
+        if (has_next)
+            pf.load_offsets(gin_off, (uint64_t) next * kTile, cnt_n);
+
+        // length sort
+        uint32_t key = 0;
+        if (tid < (int) cnt)
+            key = min((off[tid + 1] - off[tid]) >> 1, (uint32_t) kBuckets - 1);
+        const uint32_t my = sort_by_bucket(key, sm->cnt, sm->perm);
+        const bool valid = my < cnt;
+        const uint32_t rs = valid ? (uint32_t) ((uintptr_t) (a.in + off[my]) - sp_pa) : 0;
+        const uint32_t re = valid ? (uint32_t) ((uintptr_t) (a.in + off[my + 1]) - sp_pa) : 0;
+
+        // sizing (E1 / the framing choice of E3)
+        EncSize z = {0, 0, true};
+        if (valid)
+        {
+            z = sp_staged ? size_string(a, EncLds{sm->in}, rs, re, sm->len)
+                          : size_string(a, EncGlb{(const QH_GLB uint32_t *) sp_pa},
+                                        rs, re, sm->len);
+            sm->size[my] = z.size;
+        }
+        if (has_next)
+            pf.store_offsets(sm->off[cur ^ 1], cnt_n);
+        __syncthreads();
+
+        // scan in string order, publish the aggregate, prefetch the first
+        // look-back poll
+        const uint32_t sz_t = tid < (int) cnt ? sm->size[tid] : 0;
+        uint32_t total;
+        const uint32_t ex_t = block_excl_scan(sz_t, &sm->scr, &total);
+        sm->excl[tid] = ex_t;
+        publish_aggregate(a.c, tile, total);
+        LbPoll pl;
+        if (!(a.c.dbg & kDbgNoLookback))
+            look_back_load(a.c, (int64_t) tile - 1, known_tile, known_incl, &pl);
+        const bool staged_out = total + 64 <= (uint32_t) kEncOutCap;
+        if (staged_out)
+        {
+            QH_LDS u32x4 *o4 = (QH_LDS u32x4 *) sm->out;
+            const uint32_t n16 = (total + 16 + 15) / 16 + 1;
+            for (uint32_t i = tid; i < n16; i += kTile)
+                o4[i] = (u32x4){0, 0, 0, 0};
+        }
+        __syncthreads();
+
+        // next tile's input: issue the loads now, land them after packing
+        uintptr_t nx_pa = 0;
+        uint32_t nx_n16 = 0, nx_staged = 0;
+        if (has_next)
+        {
+            Span t = tile_span(a.in, sm->off[cur ^ 1], cnt_n, kEncInCap);
+            nx_pa = t.pa;
+            nx_n16 = t.n16;
+            nx_staged = t.staged;
+            if (nx_staged)
+                pf.load_chunks(nx_pa, nx_n16);
+        }
+
+        // pack (E2 / E3) into the LDS output stage
+        const uint32_t myex = valid ? sm->excl[my] : 0;
+        if (staged_out && valid && !(a.c.dbg & kDbgNoCodec))
+        {
+            Packer<PackLds> pk;
+            pk.sink.stage = sm->out;
+            pk.init(16 + myex, 16 + myex + z.size);
+            if (sp_staged)
+                emit_string(EncLds{sm->in}, rs, re, a.mode, z.huff, z.plen,
+                            sm->enc, pk);
+            else
+                emit_string(EncGlb{(const QH_GLB uint32_t *) sp_pa}, rs, re,
+                            a.mode, z.huff, z.plen, sm->enc, pk);
+        }
+
+        const uint64_t base = (a.c.dbg & kDbgNoLookback) ? (uint64_t) tile << 16
+                            : look_back(a.c, tile, total, &sm->scr, pl,
+                                        known_tile, known_incl);
+        known_tile = tile;                        // this WG's next tile is
+        known_incl = base + total;                // tile + G: it knows this
+        __syncthreads();
+
+        if (!(a.c.dbg & kDbgNoStore))
+        {
+            if (staged_out)
+                copy_out(sm->out, a.out + base, total);
+            else if (valid)
+            {
+                // positions relative to a 4-byte aligned base under a.out
+                const uint32_t adj = (uint32_t) ((uintptr_t) a.out & 3);
+                Packer<PackGlb> pk;
+                pk.sink.out = a.out - adj;
+                const uint32_t p0 = adj + (uint32_t) base + myex;
+                pk.init(p0, p0 + z.size);
+                if (sp_staged)
+                    emit_string(EncLds{sm->in}, rs, re, a.mode, z.huff,
+                                z.plen, sm->enc, pk);
+                else
+                    emit_string(EncGlb{(const QH_GLB uint32_t *) sp_pa}, rs,
+                                re, a.mode, z.huff, z.plen, sm->enc, pk);
+            }
+            QH_GLB uint32_t *gout_off = glb(a.out_off);
+            if (tid < (int) cnt)
+                gout_off[s0 + tid] = (uint32_t) (base + ex_t);
+            if (tile == a.c.n_tiles - 1 && tid == 0)
+                gout_off[a.n] = (uint32_t) (base + total);
+        }
+        if (!has_next)
+            break;
+        __syncthreads();
+        if (nx_staged)
+            pf.store_chunks<false>((QH_LDS u32x4 *) sm->in, nx_n16);
+        tile = next;
+        cnt = cnt_n;
+        sp_pa = nx_pa;
+        sp_n16 = nx_n16;
+        sp_staged = nx_staged;
+        cur ^= 1;
+    }
+}
+
+hipError_t
+launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st)
+{
+    hipLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(kTile), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t
+encode_occupancy(int *blocks_per_cu)
+{
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        blocks_per_cu, reinterpret_cast<const void *>(qhuff_encode_kernel),
+        kTile, 0);
+}
+
+size_t
+encode_lds_bytes()
+{
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(qhuff_encode_kernel))
+            != hipSuccess)
+        return 0;
+    return fa.sharedSizeBytes;
+}
+
+}  // namespace qhuff

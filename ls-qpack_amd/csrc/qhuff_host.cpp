@@ -1,0 +1,593 @@
+// qhuff_host.cpp -- host side of the C-ABI in include/qhuff.h: context
+// (tables uploaded once, look-back workspace, error word, grid sizing),
+// device-pointer batch calls, the pinned host-memory path, per-string
+// mirrors of the reference entry points, and host-only helpers.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+
+#include "qhuff_kernels.h"
+
+// ---------------------------------------------------------------------------
+// host side: context, C-ABI
+
+using namespace qhuff;
+
+struct DevTables
+{
+    uint32_t win[kWinSize];              // 16-byte aligned (copied as uint4)
+    uint2 enc[257];                      // {code, bits}
+    uint16_t sorted[257];
+};
+
+struct qhuff_ctx
+{
+    int device;
+    int n_cu;
+    uint32_t enc_grid_max, dec_grid_max; // resident workgroups (persistent)
+    hipStream_t own_stream;
+    DevTables *tab;                      // device
+    LongParams lp;
+    unsigned long long *flags;           // device, cap_tiles entries
+    uint32_t *err;                       // device error word
+    uint64_t cap_tiles;
+    uint32_t epoch;
+    uint32_t dbg;                        // QHUFF_DEBUG ablation switches
+    // host-path staging
+    uint8_t *h_stage;                    // pinned
+    size_t h_stage_cap;
+    uint8_t *d_stage;
+    size_t d_stage_cap;
+    char err_msg[256];
+};
+
+// blocks per CU that are certainly co-resident: the occupancy answer, no more
+// than the LDS allows at a 2 KiB allocation granule, and at least 1
+static int
+resident_blocks(int api, size_t lds_bytes, const hipDeviceProp_t &prop)
+{
+    const size_t gran = 2048;
+    size_t per_cu = prop.maxSharedMemoryPerMultiProcessor
+                  ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
+    size_t rounded = (lds_bytes + gran - 1) / gran * gran;
+    int by_lds = rounded ? (int) (per_cu / rounded) : api;
+    int b = api < by_lds ? api : by_lds;
+    return b < 1 ? 1 : b;
+}
+
+static int
+fail(qhuff_ctx *c, hipError_t e, const char *what)
+{
+    if (c)
+        snprintf(c->err_msg, sizeof(c->err_msg), "%s: %s", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? QHUFF_ENOMEM : QHUFF_EDEVICE;
+}
+
+#define HIPCHK(c, call)                                                      \
+    do {                                                                     \
+        hipError_t e_ = (call);                                              \
+        if (e_ != hipSuccess)                                                \
+            return fail((c), e_, #call);                                     \
+    } while (0)
+
+extern "C" int
+qhuff_open(int device, qhuff_ctx **ctx_out)
+{
+    if (!ctx_out)
+        return QHUFF_EINVAL;
+    *ctx_out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return QHUFF_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return QHUFF_ENODEV;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return QHUFF_ENODEV;              // code objects are gfx950 only
+    qhuff_ctx *c = new (std::nothrow) qhuff_ctx();
+    if (!c)
+        return QHUFF_ENOMEM;
+    c->device = device;
+    HIPCHK(c, hipSetDevice(device));
+    c->n_cu = prop.multiProcessorCount;
+    HostTables *ht = new HostTables;
+    build_tables(ht);
+    DevTables dt;
+    for (int i = 0; i < 257; ++i)
+        dt.enc[i] = make_uint2(ht->code[i], ht->bits[i]);
+    memcpy(dt.win, ht->win, sizeof(dt.win));
+    memcpy(dt.sorted, ht->sorted, sizeof(dt.sorted));
+    memset(&c->lp, 0, sizeof(c->lp));
+    c->lp.n = ht->n_long;
+    memcpy(c->lp.l, ht->longc, sizeof(LongLen) * ht->n_long);
+    delete ht;
+    int rc, occ_e = 0, occ_d = 0;
+    hipError_t e = encode_occupancy(&occ_e);
+    if (e == hipSuccess)
+        e = decode_occupancy(&occ_d);
+    if (e != hipSuccess || occ_e < 1 || occ_d < 1)
+    {
+        rc = fail(c, e, "occupancy query");
+        delete c;
+        return rc ? rc : QHUFF_EDEVICE;
+    }
+    // persistent grids: every workgroup must be resident (the look-back waits
+    // on lower tiles only, which are then always running or done).  The
+    // occupancy query is checked against LDS rounded up to a conservative
+    // allocation granule, and capped by the SGPR-admission rule of
+    // MI355X_MICROARCH.md (sec. Residency and cooperative launch).
+    occ_e = resident_blocks(occ_e, encode_lds_bytes(), prop);
+    occ_d = resident_blocks(occ_d, decode_lds_bytes(), prop);
+    c->enc_grid_max = (uint32_t) (occ_e * c->n_cu);
+    c->dec_grid_max = (uint32_t) (occ_d * c->n_cu);
+    // one look-back poll covers kLbWin predecessors; with grid <= kLbWin it
+    // always reaches the workgroup's own previous tile
+    if (c->enc_grid_max > (uint32_t) kLbWin)
+        c->enc_grid_max = (uint32_t) kLbWin;
+    if (c->dec_grid_max > (uint32_t) kLbWin)
+        c->dec_grid_max = (uint32_t) kLbWin;
+    e = hipMalloc((void **) &c->tab, sizeof(DevTables));
+    if (e != hipSuccess)
+    {
+        rc = fail(c, e, "hipMalloc tables");
+        delete c;
+        return rc;
+    }
+    e = hipMemcpy(c->tab, &dt, sizeof(dt), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMalloc((void **) &c->err, sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = hipMemset(c->err, 0, sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess)
+    {
+        rc = fail(c, e, "context setup");
+        qhuff_close(c);
+        return rc;
+    }
+    c->epoch = 0;
+    {
+        const char *d = getenv("QHUFF_DEBUG");
+        c->dbg = d ? (uint32_t) strtoul(d, nullptr, 0) : 0;
+        const char *g = getenv("QHUFF_GRID_WG_PER_CU");  // tuning override
+        if (g)
+        {
+            uint32_t k = (uint32_t) strtoul(g, nullptr, 0);
+            if (k >= 1 && k <= (uint32_t) occ_e)
+                c->enc_grid_max = k * c->n_cu;
+            if (k >= 1 && k <= (uint32_t) occ_d)
+                c->dec_grid_max = k * c->n_cu;
+        }
+    }
+    *ctx_out = c;
+    return QHUFF_OK;
+}
+
+extern "C" void
+qhuff_close(qhuff_ctx *c)
+{
+    if (!c)
+        return;
+    (void) hipSetDevice(c->device);
+    if (c->own_stream)
+        (void) hipStreamSynchronize(c->own_stream);
+    (void) hipDeviceSynchronize();
+    if (c->tab)
+        (void) hipFree(c->tab);
+    if (c->flags)
+        (void) hipFree(c->flags);
+    if (c->err)
+        (void) hipFree(c->err);
+    if (c->d_stage)
+        (void) hipFree(c->d_stage);
+    if (c->h_stage)
+        (void) hipHostFree(c->h_stage);
+    if (c->own_stream)
+        (void) hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+extern "C" const char *
+qhuff_last_error(qhuff_ctx *c)
+{
+    return c ? c->err_msg : "no context";
+}
+
+extern "C" int
+qhuff_device_error(qhuff_ctx *c)
+{
+    if (!c)
+        return QHUFF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    uint32_t v = 0;
+    HIPCHK(c, hipMemcpy(&v, c->err, 4, hipMemcpyDeviceToHost));
+    if (v)
+        HIPCHK(c, hipMemset(c->err, 0, 4));
+    return (int) v;
+}
+
+extern "C" uint64_t
+qhuff_encode_bound(uint64_t in_bytes, uint32_t n, unsigned mode)
+{
+    // 30-bit longest code: ceil(30 * len / 8) per string; framing adds at
+    // most 6 bytes of prefixed length (32-bit value) per literal
+    uint64_t b = (in_bytes * 30 + 7) / 8 + n;
+    if (mode)
+        b += 6ull * n;
+    return b + 16;
+}
+
+extern "C" uint64_t
+qhuff_decode_bound(uint64_t in_bytes, uint32_t n)
+{
+    (void) n;
+    return in_bytes * 8 / 5 + 16;
+}
+
+// make room for the look-back flags of `tiles` tiles and advance the epoch
+static int
+prepare_launch(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
+{
+    if (tiles > c->cap_tiles)
+    {
+        if (c->flags)
+        {
+            HIPCHK(c, hipStreamSynchronize(st));
+            HIPCHK(c, hipFree(c->flags));
+            c->flags = nullptr;
+        }
+        uint64_t cap = tiles < 4096 ? 4096 : tiles;
+        HIPCHK(c, hipMalloc((void **) &c->flags, cap * 8));
+        HIPCHK(c, hipMemsetAsync(c->flags, 0, cap * 8, st));
+        c->cap_tiles = cap;
+    }
+    c->epoch = (c->epoch + 1) & kEpochMask;
+    if (c->epoch == 0)
+    {
+        // wrapped: stale flags could alias the new epoch
+        HIPCHK(c, hipMemsetAsync(c->flags, 0, c->cap_tiles * 8, st));
+        c->epoch = 1;
+    }
+    return QHUFF_OK;
+}
+
+static Coord
+coord(qhuff_ctx *c, uint64_t tiles)
+{
+    Coord k;
+    k.flags = c->flags;
+    k.err = c->err;
+    k.epoch = c->epoch;
+    k.n_tiles = (uint32_t) tiles;
+    k.dbg = c->dbg;
+    return k;
+}
+
+extern "C" int
+qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
+                   uint32_t n, unsigned mode, uint8_t *out, uint32_t *out_off,
+                   void *stream)
+{
+    if (!c || !in_off || !out_off || (n && (!in || !out)))
+        return QHUFF_EINVAL;
+    if (mode != 0 && mode != 3 && mode != 5 && mode != 7)
+        return QHUFF_EINVAL;
+    hipStream_t st = (hipStream_t) stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n == 0)
+    {
+        HIPCHK(c, hipMemsetAsync(out_off, 0, 4, st));
+        return QHUFF_OK;
+    }
+    uint64_t tiles = (n + kTile - 1) / kTile;
+    int rc = prepare_launch(c, tiles, st);
+    if (rc)
+        return rc;
+    EncArgs a;
+    a.in = in;
+    a.in_off = in_off;
+    a.out = out;
+    a.out_off = out_off;
+    a.enc = c->tab->enc;
+    a.n = n;
+    a.mode = mode;
+    a.c = coord(c, tiles);
+    uint32_t grid = (uint32_t) (tiles < c->enc_grid_max ? tiles : c->enc_grid_max);
+    HIPCHK(c, launch_encode(a, grid, st));
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
+                   uint32_t n, uint8_t *out, uint32_t *out_off,
+                   uint8_t *status, void *stream)
+{
+    if (!c || !in_off || !out_off || (n && (!in || !out || !status)))
+        return QHUFF_EINVAL;
+    hipStream_t st = (hipStream_t) stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n == 0)
+    {
+        HIPCHK(c, hipMemsetAsync(out_off, 0, 4, st));
+        return QHUFF_OK;
+    }
+    uint64_t tiles = (n + kTile - 1) / kTile;
+    int rc = prepare_launch(c, tiles, st);
+    if (rc)
+        return rc;
+    DecArgs a;
+    a.in = in;
+    a.in_off = in_off;
+    a.out = out;
+    a.out_off = out_off;
+    a.status = status;
+    a.win = c->tab->win;
+    a.sorted = c->tab->sorted;
+    a.n = n;
+    a.c = coord(c, tiles);
+    a.lp = c->lp;
+    uint32_t grid = (uint32_t) (tiles < c->dec_grid_max ? tiles : c->dec_grid_max);
+    HIPCHK(c, launch_decode(a, grid, st));
+    return QHUFF_OK;
+}
+
+// ---- host-memory path ------------------------------------------------------
+
+static int
+ensure_stage(qhuff_ctx *c, size_t bytes)
+{
+    if (bytes > c->h_stage_cap)
+    {
+        if (c->h_stage)
+            (void) hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->h_stage_cap = 0;
+        HIPCHK(c, hipHostMalloc((void **) &c->h_stage, bytes));
+        c->h_stage_cap = bytes;
+    }
+    if (bytes > c->d_stage_cap)
+    {
+        if (c->d_stage)
+            (void) hipFree(c->d_stage);
+        c->d_stage = nullptr;
+        c->d_stage_cap = 0;
+        HIPCHK(c, hipMalloc((void **) &c->d_stage, bytes));
+        c->d_stage_cap = bytes;
+    }
+    return QHUFF_OK;
+}
+
+static inline size_t
+up16(size_t x)
+{
+    return (x + 15) & ~(size_t) 15;
+}
+
+// layout in both stages: [in bytes | in_off | out bytes | out_off | status]
+static int
+host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
+           uint32_t n, unsigned mode, uint8_t *out, uint32_t *out_off,
+           uint8_t *status)
+{
+    if (!c || !in_off || !out_off || (n && (!in || !out)) || (!enc && n && !status))
+        return QHUFF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t a0 = in_off[0], in_bytes = (uint64_t) in_off[n] - a0;
+    const uint64_t ob = enc ? qhuff_encode_bound(in_bytes, n, mode)
+                            : qhuff_decode_bound(in_bytes, n);
+    if (ob > 0xffffffffull)
+        return QHUFF_ERANGE;
+    size_t o_in = 0, o_off = up16(in_bytes), o_out = o_off + up16(4ull * (n + 1));
+    size_t o_oo = o_out + up16(ob), o_st = o_oo + up16(4ull * (n + 1));
+    size_t total = o_st + up16(n ? n : 1);
+    int rc = ensure_stage(c, total);
+    if (rc)
+        return rc;
+    hipStream_t st = c->own_stream;
+    memcpy(c->h_stage + o_in, in + a0, in_bytes);
+    uint32_t *hoff = (uint32_t *) (c->h_stage + o_off);
+    for (uint32_t i = 0; i <= n; ++i)
+        hoff[i] = in_off[i] - (uint32_t) a0;
+    HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, o_out,
+                             hipMemcpyHostToDevice, st));
+    if (enc)
+        rc = qhuff_encode_batch(c, c->d_stage + o_in,
+                                (const uint32_t *) (c->d_stage + o_off), n,
+                                mode, c->d_stage + o_out,
+                                (uint32_t *) (c->d_stage + o_oo), st);
+    else
+        rc = qhuff_decode_batch(c, c->d_stage + o_in,
+                                (const uint32_t *) (c->d_stage + o_off), n,
+                                c->d_stage + o_out,
+                                (uint32_t *) (c->d_stage + o_oo),
+                                c->d_stage + o_st, st);
+    if (rc)
+        return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_stage + o_oo, c->d_stage + o_oo,
+                             4ull * (n + 1), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    memcpy(out_off, c->h_stage + o_oo, 4ull * (n + 1));
+    uint64_t ot = out_off[n];
+    size_t tail = enc ? 0 : up16(n);
+    HIPCHK(c, hipMemcpyAsync(c->h_stage + o_out, c->d_stage + o_out, ot,
+                             hipMemcpyDeviceToHost, st));
+    if (!enc && n)
+        HIPCHK(c, hipMemcpyAsync(c->h_stage + o_st, c->d_stage + o_st, tail,
+                                 hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    {
+        uint32_t v = 0;
+        HIPCHK(c, hipMemcpy(&v, c->err, 4, hipMemcpyDeviceToHost));
+        if (v)
+        {
+            (void) hipMemset(c->err, 0, 4);
+            snprintf(c->err_msg, sizeof(c->err_msg), "device error %u", v);
+            return QHUFF_EDEVICE;
+        }
+    }
+    memcpy(out, c->h_stage + o_out, ot);
+    if (!enc && n)
+        memcpy(status, c->h_stage + o_st, n);
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_encode_batch_host(qhuff_ctx *c, const uint8_t *in,
+                        const uint32_t *in_off, uint32_t n, unsigned mode,
+                        uint8_t *out, uint32_t *out_off)
+{
+    if (mode != 0 && mode != 3 && mode != 5 && mode != 7)
+        return QHUFF_EINVAL;
+    return host_batch(c, true, in, in_off, n, mode, out, out_off, nullptr);
+}
+
+extern "C" int
+qhuff_decode_batch_host(qhuff_ctx *c, const uint8_t *in,
+                        const uint32_t *in_off, uint32_t n, uint8_t *out,
+                        uint32_t *out_off, uint8_t *status)
+{
+    return host_batch(c, false, in, in_off, n, 0, out, out_off, status);
+}
+
+// ---- per-string mirrors -----------------------------------------------------
+
+extern "C" int
+qhuff_enc_enc_str(qhuff_ctx *c, unsigned prefix_bits, unsigned char *dst,
+                  size_t dst_len, const unsigned char *str, unsigned str_len)
+{
+    if (!c || !dst || (!str && str_len) || (prefix_bits != 3
+            && prefix_bits != 5 && prefix_bits != 7))
+        return -1;
+    uint32_t off[2] = {0, str_len};
+    uint64_t bound = qhuff_encode_bound(str_len, 1, prefix_bits);
+    unsigned char *tmp = (unsigned char *) malloc(bound);
+    unsigned char dummy = 0;
+    uint32_t oo[2];
+    if (!tmp)
+        return -1;
+    int rc = qhuff_encode_batch_host(c, str_len ? str : &dummy, off, 1,
+                                     prefix_bits, tmp, oo);
+    int r = -1;
+    if (rc == QHUFF_OK && oo[1] <= dst_len)
+    {
+        // keep dst[0] bits above the H bit (lsqpack.c:852, 863)
+        unsigned char keep = dst[0] & (unsigned char) ~((1u << (prefix_bits + 1)) - 1);
+        memcpy(dst, tmp, oo[1]);
+        dst[0] |= keep;
+        r = (int) oo[1];
+    }
+    free(tmp);
+    return r;
+}
+
+extern "C" unsigned
+qhuff_enc_str_size(qhuff_ctx *c, const unsigned char *str, unsigned str_len)
+{
+    if (!c || (!str && str_len))
+        return 0;
+    uint32_t off[2] = {0, str_len};
+    uint64_t bound = qhuff_encode_bound(str_len, 1, 0);
+    unsigned char *tmp = (unsigned char *) malloc(bound);
+    unsigned char dummy = 0;
+    uint32_t oo[2] = {0, 0};
+    if (!tmp)
+        return 0;
+    int rc = qhuff_encode_batch_host(c, str_len ? str : &dummy, off, 1, 0, tmp,
+                                     oo);
+    free(tmp);
+    return rc == QHUFF_OK ? oo[1] : 0;
+}
+
+extern "C" struct qhuff_decode_retval
+qhuff_huff_decode(qhuff_ctx *c, const unsigned char *src, int src_len,
+                  unsigned char *dst, int dst_len)
+{
+    struct qhuff_decode_retval rv = {QHUFF_HUFF_DEC_ERROR, 0, 0};
+    if (!c || src_len < 0 || dst_len < 0 || (!src && src_len))
+        return rv;
+    uint32_t off[2] = {0, (uint32_t) src_len};
+    uint64_t bound = qhuff_decode_bound((uint64_t) src_len, 1);
+    unsigned char *tmp = (unsigned char *) malloc(bound);
+    unsigned char dummy = 0;
+    uint32_t oo[2] = {0, 0};
+    uint8_t status = QHUFF_DEC_ERROR;
+    if (!tmp)
+        return rv;
+    int rc = qhuff_decode_batch_host(c, src_len ? src : &dummy, off, 1, tmp,
+                                     oo, &status);
+    if (rc == QHUFF_OK && status == QHUFF_DEC_OK)
+    {
+        if (oo[1] <= (uint32_t) dst_len)
+        {
+            memcpy(dst, tmp, oo[1]);
+            rv.status = QHUFF_HUFF_DEC_OK;
+            rv.n_dst = oo[1];
+            rv.n_src = (unsigned) src_len;
+        }
+        else
+            rv.status = QHUFF_HUFF_DEC_END_DST;
+    }
+    free(tmp);
+    return rv;
+}
+
+// ---- host helpers --------------------------------------------------------------
+
+extern "C" int
+qhuff_shard_cuts(const uint32_t *in_off, uint32_t n, uint32_t g,
+                 uint32_t *cuts)
+{
+    if (!in_off || !cuts || g == 0)
+        return QHUFF_EINVAL;
+    const uint64_t a = in_off[0], tot = (uint64_t) in_off[n] - a;
+    cuts[0] = 0;
+    uint32_t i = 0;
+    for (uint32_t k = 1; k < g; ++k)
+    {
+        uint64_t target = a + tot * k / g;
+        // first string index whose start offset reaches the target
+        uint32_t lo = i, hi = n;
+        while (lo < hi)
+        {
+            uint32_t mid = lo + (hi - lo) / 2;
+            if (in_off[mid] < target)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        i = lo;
+        cuts[k] = i;
+    }
+    cuts[g] = n;
+    return QHUFF_OK;
+}
+
+extern "C" uint64_t
+qhuff_synth_batch(uint64_t seed, uint32_t n, uint32_t min_len,
+                  uint32_t max_len, const uint8_t *alphabet,
+                  uint32_t alphabet_len, uint8_t *data, uint32_t *in_off)
+{
+    uint64_t x = seed ? seed : 0x9E3779B97F4A7C15ull;
+    uint64_t pos = 0;
+    const uint32_t span = max_len - min_len + 1;
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        in_off[i] = (uint32_t) pos;
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        uint32_t len = min_len + (uint32_t) (x % span);
+        for (uint32_t k = 0; k < len; ++k)
+        {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            data[pos++] = alphabet[x % alphabet_len];
+        }
+    }
+    in_off[n] = (uint32_t) pos;
+    return pos;
+}

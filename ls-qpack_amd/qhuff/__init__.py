@@ -10,7 +10,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)                 # .../ls-qpack_amd
-LIB_PATH = os.path.join(PKG_ROOT, "libqhuff.so")
+LIB_PATH = os.environ.get("QHUFF_LIB") or os.path.join(PKG_ROOT, "libqhuff.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "qhuff.h")
 
 OK = 0
@@ -25,7 +25,7 @@ EXPORTS = (
     "qhuff_encode_batch", "qhuff_decode_batch", "qhuff_encode_batch_host",
     "qhuff_decode_batch_host", "qhuff_enc_enc_str", "qhuff_enc_str_size",
     "qhuff_huff_decode", "qhuff_last_error", "qhuff_shard_cuts",
-    "qhuff_synth_batch",
+    "qhuff_synth_batch", "qhuff_device_error",
 )
 
 
@@ -79,6 +79,8 @@ def lib():
         L.qhuff_last_error.argtypes = [vp]
         L.qhuff_shard_cuts.restype = C.c_int
         L.qhuff_shard_cuts.argtypes = [u32p, C.c_uint32, C.c_uint32, u32p]
+        L.qhuff_device_error.restype = C.c_int
+        L.qhuff_device_error.argtypes = [vp]
         L.qhuff_synth_batch.restype = C.c_uint64
         L.qhuff_synth_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32,
                                         C.c_uint32, C.c_char_p, C.c_uint32,
@@ -153,6 +155,11 @@ class Codec:
             self.close()
         except Exception:
             pass
+
+    def device_error(self):
+        """Synchronise and return (then clear) the sticky device error word
+        (0 = none, 1 = a look-back wait gave up)."""
+        return int(lib().qhuff_device_error(self._ctx))
 
     def _check(self, rc, what):
         if rc != OK:

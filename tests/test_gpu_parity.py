@@ -50,6 +50,7 @@ def gpu_encode(codec, data, off, mode=0, pad_front=0):
     d, o = to_dev(data, off, pad_front)
     out, out_off = codec.encode(d, o, mode)
     torch.cuda.synchronize()
+    assert codec.device_error() == 0
     oo = out_off.cpu().numpy().view(np.uint32)
     return out[:int(oo[-1])].cpu().numpy(), oo
 
@@ -58,6 +59,7 @@ def gpu_decode(codec, data, off, pad_front=0):
     d, o = to_dev(data, off, pad_front)
     out, out_off, status = codec.decode(d, o)
     torch.cuda.synchronize()
+    assert codec.device_error() == 0
     oo = out_off.cpu().numpy().view(np.uint32)
     return out[:int(oo[-1])].cpu().numpy(), oo, status.cpu().numpy()
 
