@@ -169,9 +169,9 @@ def main():
     alg_enc = raw_bytes + huff_bytes + 8 * n       # in, out, in_off, out_off
     alg_dec = huff_bytes + raw_bytes + 9 * n       # + 1 B status
     if dec_ms >= enc_ms:
-        kname, kms, alg = "qhuff_decode_tile", dec_ms, alg_dec
+        kname, kms, alg = "qhuff_decode_kernel", dec_ms, alg_dec
     else:
-        kname, kms, alg = "qhuff_encode_tile", enc_ms, alg_enc
+        kname, kms, alg = "qhuff_encode_kernel", enc_ms, alg_enc
     achieved = alg / (kms * 1e-3) / 1e9
     traffic = None
     pmc_src = None

@@ -87,7 +87,9 @@ struct Packer
     }
     __device__ __forceinline__ void put(uint32_t code, uint32_t len)
     {
-        acc |= (uint64_t) code << (64 - nbits - len);
+        // len == 0 is a no-op (masked byte)
+        const uint64_t v = len ? (uint64_t) code << (64 - nbits - len) : 0;
+        acc |= v;
         nbits += len;
         if (nbits >= 32)
         {
@@ -130,23 +132,39 @@ int_len(uint32_t v, uint32_t prefix)
     return n;
 }
 
-// sum of code lengths over bytes [rs, re) (positions relative to the source)
+// valid-byte mask (4 bits) of dword d for a string [rs, re), re > rs
+__device__ __forceinline__ uint32_t
+byte_mask(uint32_t d, uint32_t d0, uint32_t dl, uint32_t rs, uint32_t re)
+{
+    uint32_t m = 0xfu;
+    m &= (d == d0) ? (0xfu << (rs & 3)) : 0xfu;
+    m &= (d == dl) ? (0xfu >> (3 - ((re - 1) & 3))) : 0xfu;
+    return m;
+}
+
+// sum of code lengths over bytes [rs, re) (positions relative to the source):
+// four independent LDS lookups per dword, masked and summed with v_sad_u8
 template <class Src>
 __device__ __forceinline__ uint32_t
 code_bits(const Src &src, uint32_t rs, uint32_t re, const QH_LDS uint8_t *s_len)
 {
     uint32_t bits = 0;
-    const uint32_t d0 = rs >> 2, d1 = (re + 3) >> 2;
-    for (uint32_t d = d0; d < d1; ++d)
+    if (re == rs)
+        return 0;
+    const uint32_t d0 = rs >> 2, dl = (re - 1) >> 2;
+    for (uint32_t d = d0; d <= dl; ++d)
     {
-        uint32_t w = src.dw(d);
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-        {
-            uint32_t p = 4 * d + b;
-            uint32_t l = s_len[(w >> (8 * b)) & 0xff];
-            bits += (p >= rs && p < re) ? l : 0;
-        }
+        const uint32_t w = src.dw(d);
+        const uint32_t l0 = s_len[w & 0xff];
+        const uint32_t l1 = s_len[(w >> 8) & 0xff];
+        const uint32_t l2 = s_len[(w >> 16) & 0xff];
+        const uint32_t l3 = s_len[w >> 24];
+        const uint32_t m = byte_mask(d, d0, dl, rs, re);
+        // expand the 4-bit mask to bytes: 0x000000ff per set bit
+        const uint32_t bm = (m & 1 ? 0xffu : 0u) | (m & 2 ? 0xff00u : 0u)
+                          | (m & 4 ? 0xff0000u : 0u) | (m & 8 ? 0xff000000u : 0u);
+        const uint32_t packed = l0 | (l1 << 8) | (l2 << 16) | (l3 << 24);
+        bits = __builtin_amdgcn_sad_u8(packed & bm, 0u, bits);
     }
     return bits;
 }
@@ -156,26 +174,26 @@ __device__ __forceinline__ void
 pack_string(const Src &src, uint32_t rs, uint32_t re, bool raw,
             const QH_LDS u32x2 *s_enc, Packer<Sink> &pk)
 {
-    const uint32_t d0 = rs >> 2, d1 = (re + 3) >> 2;
-    for (uint32_t d = d0; d < d1; ++d)
+    if (re == rs)
+        return;
+    const uint32_t d0 = rs >> 2, dl = (re - 1) >> 2;
+    for (uint32_t d = d0; d <= dl; ++d)
     {
-        uint32_t w = src.dw(d);
+        const uint32_t w = src.dw(d);
+        const uint32_t m = byte_mask(d, d0, dl, rs, re);
+        // unconditional lookups (independent LDS reads), then masked puts
+        u32x2 e[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b)
         {
-            uint32_t p = 4 * d + b;
-            if (p >= rs && p < re)
-            {
-                uint32_t c = (w >> (8 * b)) & 0xff;
-                if (raw)
-                    pk.put(c, 8);
-                else
-                {
-                    u32x2 e = s_enc[c];
-                    pk.put(e.x, e.y);
-                }
-            }
+            const uint32_t c = (w >> (8 * b)) & 0xff;
+            const u32x2 t = s_enc[c];            // always read: no branch
+            e[b].x = raw ? c : t.x;
+            e[b].y = raw ? 8u : t.y;
         }
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            pk.put(e[b].x, (m >> b) & 1 ? e[b].y : 0u);
     }
 }
 
