@@ -22,7 +22,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kTile = 256;                  // strings per tile = threads per WG
-constexpr int kBuckets = 128;               // length buckets for the tile sort
+constexpr int kBuckets = 64;                // length buckets for the tile sort
 
 // look-back flag word: [63:62] state, [61:40] epoch, [39:0] byte count
 constexpr uint64_t kFlagAgg = 1ull << 62;
@@ -46,14 +46,21 @@ struct Coord
     uint32_t epoch;                         // launch tag carried in flags
     uint32_t n_tiles;
     uint32_t dbg;
+    unsigned long long *trace;              // QHUFF_TRACE: 8 stamps per tile
 };
 
-struct LdsScratch                           // per-WG scan / look-back scratch
+// phase stamps for tools/trace_report.py (null trace: one scalar branch)
+__device__ __forceinline__ void
+stamp(const Coord &c, uint32_t tile, int slot)
 {
-    uint64_t inc[16], inv[16];
-    uint64_t wsum64[4];
+    if (c.trace && (threadIdx.x & 63) == 0)
+        c.trace[8ull * tile + slot] = slot == 0 ? __builtin_amdgcn_s_memrealtime()
+                                                : __builtin_amdgcn_s_memtime();
+}
+
+struct LdsScratch                           // per-WG scan scratch
+{
     uint32_t wsum[4];
-    uint64_t base;
 };
 
 __device__ __forceinline__ uint32_t
@@ -107,8 +114,8 @@ sort_by_bucket(uint32_t key, QH_LDS uint32_t *s_cnt, QH_LDS uint16_t *s_perm)
     __syncthreads();
     if (tid < 64)
     {
-        uint32_t a = s_cnt[2 * lane], b = s_cnt[2 * lane + 1];
-        uint32_t x = a + b;
+        const uint32_t a = s_cnt[lane];
+        uint32_t x = a;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1)
         {
@@ -116,9 +123,7 @@ sort_by_bucket(uint32_t key, QH_LDS uint32_t *s_cnt, QH_LDS uint16_t *s_perm)
             if (lane >= d)
                 x += y;
         }
-        uint32_t ex = x - a - b;
-        s_cnt[2 * lane] = ex;
-        s_cnt[2 * lane + 1] = ex + a;
+        s_cnt[lane] = x - a;
     }
     __syncthreads();
     s_perm[s_cnt[key] + pos] = (uint16_t) tid;
@@ -126,129 +131,102 @@ sort_by_bucket(uint32_t key, QH_LDS uint32_t *s_cnt, QH_LDS uint16_t *s_perm)
     return s_perm[tid];
 }
 
-// Look-back window: kLbWin predecessors per poll, kLbK flags per thread.
-constexpr int kLbK = 4;
-constexpr int kLbWin = kLbK * kTile;
+// Look-back by ONE wave (the store wave, see the kernels' role split):
+// kLbK flags per lane, kLbWin predecessors per poll.  Position q of the
+// window (q = 64k + lane) is tile j - q.
+constexpr int kLbK = 16;
+constexpr int kLbWin = kLbK * 64;
 
-// Look-back state of one tile: the flags of its kLbWin nearest predecessors
-// (thread tid holds positions tid + 256k, position p = tile - 1 - p), loaded
-// early so the poll latency overlaps other work.
-struct LbPoll
-{
-    uint64_t f[kLbK];
-};
-
-// known_tile / known_incl: a predecessor whose inclusive prefix this
-// workgroup already knows (its own previous tile, t - gridDim.x), or
-// known_tile = -1.  With gridDim.x <= kLbWin one poll always reaches it.
-__device__ __forceinline__ void
-look_back_load(const Coord &c, int64_t j, int64_t known_tile,
-               uint64_t known_incl, LbPoll *pl)
-{
-    const uint64_t ep = (uint64_t) c.epoch << 40;
-#pragma unroll
-    for (int k = 0; k < kLbK; ++k)
-    {
-        const int64_t idx = j - threadIdx.x - kTile * k;
-        uint64_t f;
-        if (idx < 0)
-            f = kFlagInc | ep;                       // before tile 0: 0
-        else if (idx == known_tile)
-            f = kFlagInc | ep | (known_incl & kValMask);
-        else
-            f = __hip_atomic_load(&c.flags[idx], __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-        pl->f[k] = f;
-    }
-}
-
-// Decoupled look-back.  Returns the exclusive byte prefix of `tile` and
-// publishes its inclusive value.  `pl` holds the first poll (from
-// look_back_load(tile - 1, ...)).  Uniform control flow: every thread of the
-// workgroup must call it.
+// known_tile / known_incl: a predecessor whose inclusive prefix the calling
+// workgroup already knows (its own previous tile), or known_tile = -1.  With
+// gridDim.x <= kLbWin one poll always reaches it.  Returns the exclusive
+// byte prefix of `tile` and publishes its inclusive value (lane 0).
 __device__ __forceinline__ uint64_t
-look_back(const Coord &c, uint32_t tile, uint64_t agg, QH_LDS LdsScratch *scr,
-          LbPoll pl, int64_t known_tile, uint64_t known_incl)
+look_back_wave(const Coord &c, uint32_t tile, uint64_t agg,
+               int64_t known_tile, uint64_t known_incl)
 {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lane = threadIdx.x & 63;
     const uint64_t ep = (uint64_t) c.epoch << 40;
     uint64_t excl = 0;
     int64_t j = (int64_t) tile - 1;
     uint32_t spins = 0;
     while (j >= 0)
     {
-        // nearest inclusive position F and validity up to it
-        bool any_inc = false;
+        uint64_t f[kLbK];
 #pragma unroll
         for (int k = 0; k < kLbK; ++k)
         {
-            const uint64_t f = pl.f[k];
-            const bool valid = ((f >> 40) & kEpochMask) == c.epoch
-                             && (f >> 62) != 0;
-            const bool inc = valid && (f >> 62) == 2;
-            const uint64_t incm = __ballot(inc), invm = __ballot(!valid);
-            if (lane == 0)
-            {
-                scr->inc[4 * k + wave] = incm;
-                scr->inv[4 * k + wave] = invm;
-            }
+            const int64_t idx = j - lane - 64 * k;
+            if (idx < 0)
+                f[k] = kFlagInc | ep;                    // before tile 0
+            else if (idx == known_tile)
+                f[k] = kFlagInc | ep | (known_incl & kValMask);
+            else
+                f[k] = __hip_atomic_load(&c.flags[idx], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
         }
-        __syncthreads();
-        int F = kLbWin;
+        int F = kLbWin;                  // nearest inclusive position
+        uint64_t inv[kLbK];
 #pragma unroll
-        for (int q = 4 * kLbK - 1; q >= 0; --q)
+        for (int k = kLbK - 1; k >= 0; --k)
         {
-            const uint64_t im = scr->inc[q];
+            const bool valid = ((f[k] >> 40) & kEpochMask) == c.epoch
+                             && (f[k] >> 62) != 0;
+            const bool inc = valid && (f[k] >> 62) == 2;
+            const uint64_t im = __ballot(inc);
+            inv[k] = __ballot(!valid);
             if (im)
-                F = 64 * q + __builtin_ctzll(im);
+                F = 64 * k + __builtin_ctzll(im);
         }
-        any_inc = F < kLbWin;
-        const int fcap = any_inc ? F : kLbWin - 1;
+        const int fcap = F < kLbWin ? F : kLbWin - 1;
         bool bad = false;
 #pragma unroll
-        for (int q = 0; q < 4 * kLbK; ++q)
+        for (int k = 0; k < kLbK; ++k)
         {
-            const int lim = fcap - 64 * q;
+            const int lim = fcap - 64 * k;
             const uint64_t m = lim >= 63 ? ~0ull
                              : (lim < 0 ? 0ull : ((2ull << lim) - 1));
-            bad |= (scr->inv[q] & m) != 0;
+            bad |= (inv[k] & m) != 0;
         }
-        __syncthreads();
         if (bad)
         {
             if (++spins > kSpinLimit)
             {
-                if (tid == 0)
+                if (lane == 0)
                     atomicOr(c.err, kErrSpin);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
-            look_back_load(c, j, known_tile, known_incl, &pl);
             continue;
         }
         uint64_t mine = 0;
 #pragma unroll
         for (int k = 0; k < kLbK; ++k)
-            mine += (tid + kTile * k <= F) ? (pl.f[k] & kValMask) : 0;
+            mine += (lane + 64 * k <= F) ? (f[k] & kValMask) : 0;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1)
             mine += __shfl_xor(mine, d, 64);
-        if (lane == 0)
-            scr->wsum64[wave] = mine;
-        __syncthreads();
-        excl += scr->wsum64[0] + scr->wsum64[1] + scr->wsum64[2]
-              + scr->wsum64[3];
-        __syncthreads();
-        if (any_inc)
+        excl += mine;
+        if (F < kLbWin)
             break;
         j -= kLbWin;
-        look_back_load(c, j, known_tile, known_incl, &pl);
     }
-    if (tid == 0)
+    if (lane == 0)
         __hip_atomic_store(&c.flags[tile],
                            kFlagInc | ep | ((excl + agg) & kValMask),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return excl;
+}
+
+// the store wave (wave 3) issues every global store and the look-back; the
+// load waves (0..2) issue every prefetch load and never store, so their
+// s_waitcnt vmcnt never drains a store (vmcnt counts loads and stores in
+// issue order, MI355X_MICROARCH.md sec. per-instruction constants)
+constexpr int kLoadThreads = 192;
+__device__ __forceinline__ bool
+is_store_wave()
+{
+    return threadIdx.x >= kLoadThreads;
 }
 
 // Next-tile prefetch: offsets and up to NCH 16-byte input chunks per thread
@@ -256,31 +234,33 @@ look_back(const Coord &c, uint32_t tile, uint64_t agg, QH_LDS LdsScratch *scr,
 template <int NCH>
 struct Prefetch
 {
-    uint32_t off, off_end;
+    uint32_t off0, off1;            // two offsets per load thread (257 needed)
     u32x4 ch[NCH];
 
     __device__ __forceinline__ void load_offsets(const QH_GLB uint32_t *in_off,
                                                  uint64_t s0, uint32_t cnt)
     {
-        const int tid = threadIdx.x;
-        off = tid < (int) cnt ? in_off[s0 + tid] : 0;
-        off_end = tid == 0 ? in_off[s0 + cnt] : 0;
+        const int tid = threadIdx.x;       // load waves only
+        off0 = tid <= (int) cnt ? in_off[s0 + tid] : 0;
+        const int t1 = tid + kLoadThreads;
+        off1 = t1 <= (int) cnt ? in_off[s0 + t1] : 0;
     }
     __device__ __forceinline__ void store_offsets(QH_LDS uint32_t *s_off,
                                                   uint32_t cnt) const
     {
         const int tid = threadIdx.x;
-        if (tid < (int) cnt)
-            s_off[tid] = off;
-        if (tid == 0)
-            s_off[cnt] = off_end;
+        if (tid <= (int) cnt)
+            s_off[tid] = off0;
+        const int t1 = tid + kLoadThreads;
+        if (t1 <= (int) cnt)
+            s_off[t1] = off1;
     }
     __device__ __forceinline__ void load_chunks(uintptr_t pa, uint32_t n16)
     {
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
         {
-            uint32_t i = threadIdx.x + k * kTile;
+            uint32_t i = threadIdx.x + k * kLoadThreads;
             if (i < n16)
                 ch[k] = ((const QH_GLB u32x4 *) pa)[i];
         }
@@ -292,7 +272,7 @@ struct Prefetch
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
         {
-            uint32_t i = threadIdx.x + k * kTile;
+            uint32_t i = threadIdx.x + k * kLoadThreads;
             if (i < n16)
             {
                 u32x4 v = ch[k];
@@ -330,7 +310,7 @@ tile_span(const uint8_t *in, const QH_LDS uint32_t *s_off, uint32_t cnt,
 __device__ __forceinline__ void
 publish_aggregate(const Coord &c, uint32_t tile, uint64_t agg)
 {
-    if (threadIdx.x == 0)
+    if (threadIdx.x == kLoadThreads)        // first lane of the store wave
         __hip_atomic_store(&c.flags[tile],
                            kFlagAgg | ((uint64_t) c.epoch << 40)
                            | (agg & kValMask),
@@ -339,7 +319,8 @@ publish_aggregate(const Coord &c, uint32_t tile, uint64_t agg)
 
 // Copy `total` bytes that sit at LDS byte offset 16 (s_stage has 16 bytes of
 // pad in front) to global `dst` (any alignment) with 16-byte aligned stores;
-// the partial first/last 16-byte chunks are written byte by byte.
+// the partial first/last 16-byte chunks are written byte by byte.  Called by
+// the store wave (64 lanes).
 __device__ __forceinline__ void
 copy_out(const QH_LDS uint32_t *s_stage, uint8_t *dst, uint32_t total)
 {
@@ -352,7 +333,7 @@ copy_out(const QH_LDS uint32_t *s_stage, uint8_t *dst, uint32_t total)
     const uint32_t sh = (16 - r) & 15;       // byte shift inside the stage
     const uint32_t c0 = (16 - r) >> 4;       // 1 when r == 0, else 0
     const QH_LDS u32x4 *s4 = (const QH_LDS u32x4 *) s_stage;
-    for (uint32_t k = threadIdx.x; k < nchunk; k += kTile)
+    for (uint32_t k = threadIdx.x & 63; k < nchunk; k += 64)
     {
         u32x4 a = s4[k + c0], b = s4[k + c0 + 1];
         uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};

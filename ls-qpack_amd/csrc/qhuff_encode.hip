@@ -23,8 +23,6 @@
 
 namespace qhuff {
 
-constexpr int kEncInCap = 16 * 1024;        // staged input bytes per tile
-constexpr int kEncOutCap = 16 * 1024;       // staged output bytes per tile
 
 // source of aligned input dwords: LDS stage or global
 struct EncLds
@@ -226,21 +224,24 @@ emit_string(const Src &src, uint32_t rs, uint32_t re, uint32_t mode,
     pk.finish();
 }
 
+constexpr int kEncInCapL = 12 * 1024;       // staged input bytes per tile
+constexpr int kEncOutCapL = 12 * 1024;      // staged output bytes per tile
+
 struct EncSmem
 {
     u32x2 enc[257];
     uint8_t len[256];
     uint32_t off[2][kTile + 1];      // current / next tile offsets
     uint32_t size[kTile];
-    uint32_t excl[kTile];
+    uint32_t excl[2][kTile];         // tile offsets, by tile parity
     uint32_t cnt[kBuckets];
     uint16_t perm[kTile];
     LdsScratch scr;
-    alignas(16) uint32_t in[kEncInCap / 4 + 4];
-    alignas(16) uint32_t out[(kEncOutCap + 64) / 4];   // 16 B pad in front
+    alignas(16) uint32_t in[kEncInCapL / 4 + 4];
+    alignas(16) uint32_t out[2][(kEncOutCapL + 64) / 4];  // 16 B pad in front
 };
 
-constexpr int kEncChunks = kEncInCap / 16 / kTile;      // prefetch regs
+constexpr int kEncChunks = (kEncInCapL / 16 + kLoadThreads - 1) / kLoadThreads;
 
 // per-string sizing result
 struct EncSize
@@ -271,12 +272,71 @@ size_string(const EncArgs &a, const Src &src, uint32_t rs, uint32_t re,
     return z;
 }
 
-__global__ __launch_bounds__(kTile) void
+// the tile whose look-back / copy-out is deferred to the next iteration
+struct EncDeferred
+{
+    uint32_t tile, cnt, total, par;
+    uint32_t staged_out;
+    uintptr_t pa;              // input span (slow path)
+    uint32_t staged_in;
+};
+
+// store wave: look-back + copy-out + out_off of the deferred tile
+__device__ __forceinline__ uint64_t
+enc_finish(const EncArgs &a, QH_LDS EncSmem *sm, const EncDeferred &df,
+           int64_t *known_tile, uint64_t *known_incl)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t base = (a.c.dbg & kDbgNoLookback) ? (uint64_t) df.tile << 16
+        : look_back_wave(a.c, df.tile, df.total, *known_tile, *known_incl);
+    *known_tile = df.tile;
+    *known_incl = base + df.total;
+    if (a.c.dbg & kDbgNoStore)
+        return base;
+    const uint64_t s0 = (uint64_t) df.tile * kTile;
+    QH_GLB uint32_t *gout_off = glb(a.out_off);
+    if (df.staged_out)
+        copy_out(sm->out[df.par], a.out + base, df.total);
+    for (int t = lane; t < (int) df.cnt; t += 64)
+        gout_off[s0 + t] = (uint32_t) (base + sm->excl[df.par][t]);
+    if (df.tile == a.c.n_tiles - 1 && lane == 0)
+        gout_off[a.n] = (uint32_t) (base + df.total);
+    return base;
+}
+
+// slow path (tile output too large for the stage): every lane packs its
+// string again straight to global memory, input read from global
+__device__ __forceinline__ void
+enc_finish_slow(const EncArgs &a, QH_LDS EncSmem *sm, const EncDeferred &df,
+                uint64_t base)
+{
+    const int tid = threadIdx.x;
+    if ((a.c.dbg & kDbgNoStore) || tid >= (int) df.cnt)
+        return;
+    const QH_GLB uint32_t *gin_off = glb(a.in_off);
+    const uint64_t s0 = (uint64_t) df.tile * kTile;
+    const uint32_t o0 = gin_off[s0 + tid], o1 = gin_off[s0 + tid + 1];
+    const uintptr_t pa = (uintptr_t) (a.in + o0) & ~(uintptr_t) 3;
+    const uint32_t rs = (uint32_t) ((uintptr_t) (a.in + o0) - pa);
+    const uint32_t re = rs + (o1 - o0);
+    EncGlb src{(const QH_GLB uint32_t *) pa};
+    EncSize z = size_string(a, src, rs, re, sm->len);
+    const uint32_t adj = (uint32_t) ((uintptr_t) a.out & 3);
+    Packer<PackGlb> pk;
+    pk.sink.out = a.out - adj;
+    const uint32_t p0 = adj + (uint32_t) base + sm->excl[df.par][tid];
+    pk.init(p0, p0 + z.size);
+    emit_string(src, rs, re, a.mode, z.huff, z.plen, sm->enc, pk);
+}
+
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 qhuff_encode_kernel(EncArgs a)
 {
     __shared__ EncSmem smem;
+    __shared__ uint64_t s_base;
     QH_LDS EncSmem *sm = (QH_LDS EncSmem *) &smem;
     const int tid = threadIdx.x;
+    const bool ldw = !is_store_wave();
 
     const QH_GLB u32x2 *genc = (const QH_GLB u32x2 *) a.enc;
     const u32x2 e_t = genc[tid];
@@ -291,37 +351,46 @@ qhuff_encode_kernel(EncArgs a)
     if (tile >= a.c.n_tiles)
         return;
 
-    // prologue: offsets + input of the first tile
+    // prologue: offsets + input of the first tile (load waves)
     Prefetch<kEncChunks> pf;
     uint32_t cnt = (uint32_t) min((uint64_t) kTile, a.n - (uint64_t) tile * kTile);
-    pf.load_offsets(gin_off, (uint64_t) tile * kTile, cnt);
-    pf.store_offsets(sm->off[0], cnt);
+    if (ldw)
+    {
+        pf.load_offsets(gin_off, (uint64_t) tile * kTile, cnt);
+        pf.store_offsets(sm->off[0], cnt);
+    }
     __syncthreads();
-    Span sp0 = tile_span(a.in, sm->off[0], cnt, kEncInCap);
+    Span sp0 = tile_span(a.in, sm->off[0], cnt, kEncInCapL);
     uintptr_t sp_pa = sp0.pa;
     uint32_t sp_n16 = sp0.n16;
     uint32_t sp_staged = sp0.staged;
-    if (sp_staged)
+    if (sp_staged && ldw)
     {
         pf.load_chunks(sp_pa, sp_n16);
         pf.store_chunks<false>((QH_LDS u32x4 *) sm->in, sp_n16);
     }
-    uint32_t cur = 0;
-    int64_t known_tile = -1;                      // see look_back()
+    uint32_t cur = 0, par = 0;
+    int64_t known_tile = -1;
     uint64_t known_incl = 0;
+    bool pending = false;
+    EncDeferred df = {0, 0, 0, 0, 0, 0, 0};
 
     for (;;)
     {
         const QH_LDS uint32_t *off = sm->off[cur];
-        const uint64_t s0 = (uint64_t) tile * kTile;
         const uint32_t next = tile + G;
         const bool has_next = next < a.c.n_tiles;
         const uint32_t cnt_n = has_next
             ? (uint32_t) min((uint64_t) kTile, a.n - (uint64_t) next * kTile) : 0;
-        if (has_next)
+        if (threadIdx.x < 64)
+        {
+            stamp(a.c, tile, 0);
+            stamp(a.c, tile, 1);
+        }
+        if (has_next && ldw)
             pf.load_offsets(gin_off, (uint64_t) next * kTile, cnt_n);
 
-        // length sort
+        // 1. length sort + sizing (E1 / the framing choice of E3)
         uint32_t key = 0;
         if (tid < (int) cnt)
             key = min((off[tid + 1] - off[tid]) >> 1, (uint32_t) kBuckets - 1);
@@ -329,8 +398,6 @@ qhuff_encode_kernel(EncArgs a)
         const bool valid = my < cnt;
         const uint32_t rs = valid ? (uint32_t) ((uintptr_t) (a.in + off[my]) - sp_pa) : 0;
         const uint32_t re = valid ? (uint32_t) ((uintptr_t) (a.in + off[my + 1]) - sp_pa) : 0;
-
-        // sizing (E1 / the framing choice of E3)
         EncSize z = {0, 0, true};
         if (valid)
         {
@@ -339,49 +406,66 @@ qhuff_encode_kernel(EncArgs a)
                                         rs, re, sm->len);
             sm->size[my] = z.size;
         }
-        if (has_next)
+        if (threadIdx.x < 64)
+            stamp(a.c, tile, 2);
+        else if (!ldw)
+            stamp(a.c, tile, 3);
+        if (has_next && ldw)
             pf.store_offsets(sm->off[cur ^ 1], cnt_n);
         __syncthreads();
+        if (threadIdx.x < 64)
+            stamp(a.c, tile, 4);
 
-        // scan in string order, publish the aggregate, prefetch the first
-        // look-back poll
+        // 2. scan in string order
         const uint32_t sz_t = tid < (int) cnt ? sm->size[tid] : 0;
         uint32_t total;
         const uint32_t ex_t = block_excl_scan(sz_t, &sm->scr, &total);
-        sm->excl[tid] = ex_t;
-        publish_aggregate(a.c, tile, total);
-        LbPoll pl;
-        if (!(a.c.dbg & kDbgNoLookback))
-            look_back_load(a.c, (int64_t) tile - 1, known_tile, known_incl, &pl);
-        const bool staged_out = total + 64 <= (uint32_t) kEncOutCap;
+        sm->excl[par][tid] = ex_t;
+        const bool staged_out = total + 64 <= (uint32_t) kEncOutCapL;
         if (staged_out)
         {
-            QH_LDS u32x4 *o4 = (QH_LDS u32x4 *) sm->out;
+            QH_LDS u32x4 *o4 = (QH_LDS u32x4 *) sm->out[par];
             const uint32_t n16 = (total + 16 + 15) / 16 + 1;
             for (uint32_t i = tid; i < n16; i += kTile)
                 o4[i] = (u32x4){0, 0, 0, 0};
         }
-        __syncthreads();
 
-        // next tile's input: issue the loads now, land them after packing
+        // 3. load waves: next tile's input loads; store wave: deferred
+        //    tile's look-back + copy-out + offsets, then this aggregate
         uintptr_t nx_pa = 0;
         uint32_t nx_n16 = 0, nx_staged = 0;
         if (has_next)
         {
-            Span t = tile_span(a.in, sm->off[cur ^ 1], cnt_n, kEncInCap);
+            Span t = tile_span(a.in, sm->off[cur ^ 1], cnt_n, kEncInCapL);
             nx_pa = t.pa;
             nx_n16 = t.n16;
             nx_staged = t.staged;
-            if (nx_staged)
+            if (nx_staged && ldw)
                 pf.load_chunks(nx_pa, nx_n16);
         }
+        if (!ldw)
+            stamp(a.c, tile, 5);
+        if (pending && !ldw)
+        {
+            const uint64_t b = enc_finish(a, sm, df, &known_tile, &known_incl);
+            if ((tid & 63) == 0)
+                s_base = b;
+        }
+        if (!ldw)
+        {
+            publish_aggregate(a.c, tile, total);
+            stamp(a.c, tile, 6);
+        }
+        __syncthreads();
+        if (pending && !df.staged_out)
+            enc_finish_slow(a, sm, df, s_base);
 
-        // pack (E2 / E3) into the LDS output stage
-        const uint32_t myex = valid ? sm->excl[my] : 0;
+        // 4. pack (E2 / E3) into the LDS output stage of this parity
+        const uint32_t myex = valid ? sm->excl[par][my] : 0;
         if (staged_out && valid && !(a.c.dbg & kDbgNoCodec))
         {
             Packer<PackLds> pk;
-            pk.sink.stage = sm->out;
+            pk.sink.stage = sm->out[par];
             pk.init(16 + myex, 16 + myex + z.size);
             if (sp_staged)
                 emit_string(EncLds{sm->in}, rs, re, a.mode, z.huff, z.plen,
@@ -390,43 +474,18 @@ qhuff_encode_kernel(EncArgs a)
                 emit_string(EncGlb{(const QH_GLB uint32_t *) sp_pa}, rs, re,
                             a.mode, z.huff, z.plen, sm->enc, pk);
         }
-
-        const uint64_t base = (a.c.dbg & kDbgNoLookback) ? (uint64_t) tile << 16
-                            : look_back(a.c, tile, total, &sm->scr, pl,
-                                        known_tile, known_incl);
-        known_tile = tile;                        // this WG's next tile is
-        known_incl = base + total;                // tile + G: it knows this
+        df.tile = tile;
+        df.cnt = cnt;
+        df.total = total;
+        df.par = par;
+        df.staged_out = staged_out;
+        pending = true;
         __syncthreads();
-
-        if (!(a.c.dbg & kDbgNoStore))
-        {
-            if (staged_out)
-                copy_out(sm->out, a.out + base, total);
-            else if (valid)
-            {
-                // positions relative to a 4-byte aligned base under a.out
-                const uint32_t adj = (uint32_t) ((uintptr_t) a.out & 3);
-                Packer<PackGlb> pk;
-                pk.sink.out = a.out - adj;
-                const uint32_t p0 = adj + (uint32_t) base + myex;
-                pk.init(p0, p0 + z.size);
-                if (sp_staged)
-                    emit_string(EncLds{sm->in}, rs, re, a.mode, z.huff,
-                                z.plen, sm->enc, pk);
-                else
-                    emit_string(EncGlb{(const QH_GLB uint32_t *) sp_pa}, rs,
-                                re, a.mode, z.huff, z.plen, sm->enc, pk);
-            }
-            QH_GLB uint32_t *gout_off = glb(a.out_off);
-            if (tid < (int) cnt)
-                gout_off[s0 + tid] = (uint32_t) (base + ex_t);
-            if (tile == a.c.n_tiles - 1 && tid == 0)
-                gout_off[a.n] = (uint32_t) (base + total);
-        }
+        if (threadIdx.x < 64)
+            stamp(a.c, tile, 7);
         if (!has_next)
             break;
-        __syncthreads();
-        if (nx_staged)
+        if (nx_staged && ldw)
             pf.store_chunks<false>((QH_LDS u32x4 *) sm->in, nx_n16);
         tile = next;
         cnt = cnt_n;
@@ -434,7 +493,17 @@ qhuff_encode_kernel(EncArgs a)
         sp_n16 = nx_n16;
         sp_staged = nx_staged;
         cur ^= 1;
+        par ^= 1;
     }
+    if (!ldw)
+    {
+        const uint64_t b = enc_finish(a, sm, df, &known_tile, &known_incl);
+        if ((tid & 63) == 0)
+            s_base = b;
+    }
+    __syncthreads();
+    if (!df.staged_out)
+        enc_finish_slow(a, sm, df, s_base);
 }
 
 hipError_t

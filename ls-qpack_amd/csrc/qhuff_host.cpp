@@ -38,6 +38,9 @@ struct qhuff_ctx
     uint64_t cap_tiles;
     uint32_t epoch;
     uint32_t dbg;                        // QHUFF_DEBUG ablation switches
+    const char *trace_path;              // QHUFF_TRACE phase-stamp dump
+    unsigned long long *trace;           // device, trace_cap stamps
+    uint64_t trace_cap;
     // host-path staging
     uint8_t *h_stage;                    // pinned
     size_t h_stage_cap;
@@ -155,6 +158,7 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     {
         const char *d = getenv("QHUFF_DEBUG");
         c->dbg = d ? (uint32_t) strtoul(d, nullptr, 0) : 0;
+        c->trace_path = getenv("QHUFF_TRACE");
         const char *g = getenv("QHUFF_GRID_WG_PER_CU");  // tuning override
         if (g)
         {
@@ -186,6 +190,8 @@ qhuff_close(qhuff_ctx *c)
         (void) hipFree(c->err);
     if (c->d_stage)
         (void) hipFree(c->d_stage);
+    if (c->trace)
+        (void) hipFree(c->trace);
     if (c->h_stage)
         (void) hipHostFree(c->h_stage);
     if (c->own_stream)
@@ -259,15 +265,59 @@ prepare_launch(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
 }
 
 static Coord
-coord(qhuff_ctx *c, uint64_t tiles)
+coord(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
 {
     Coord k;
+    k.trace = nullptr;
+    if (c->trace_path)
+    {
+        if (c->trace_cap < 8 * tiles)
+        {
+            if (c->trace)
+                (void) hipFree(c->trace);
+            c->trace = nullptr;
+            c->trace_cap = 0;
+            if (hipMalloc((void **) &c->trace, 64 * tiles) == hipSuccess)
+                c->trace_cap = 8 * tiles;
+        }
+        if (c->trace)
+        {
+            (void) hipMemsetAsync(c->trace, 0, 64 * tiles, st);
+            k.trace = c->trace;
+        }
+    }
     k.flags = c->flags;
     k.err = c->err;
     k.epoch = c->epoch;
     k.n_tiles = (uint32_t) tiles;
     k.dbg = c->dbg;
     return k;
+}
+
+// diagnostic only (QHUFF_TRACE=path): synchronises, appends one record
+// {u32 'QTRC', kind, tiles, grid, tiles * 8 u64 stamps} to the file
+static void
+dump_trace(qhuff_ctx *c, uint32_t kind, uint64_t tiles, uint32_t grid,
+           hipStream_t st)
+{
+    if (!c->trace || c->trace_cap < 8 * tiles)
+        return;
+    unsigned long long *h = (unsigned long long *) malloc(64 * tiles);
+    if (!h)
+        return;
+    if (hipMemcpyAsync(h, c->trace, 64 * tiles, hipMemcpyDeviceToHost, st) == hipSuccess
+            && hipStreamSynchronize(st) == hipSuccess)
+    {
+        FILE *f = fopen(c->trace_path, "ab");
+        if (f)
+        {
+            const uint32_t hdr[4] = {0x43525451u, kind, (uint32_t) tiles, grid};
+            (void) fwrite(hdr, sizeof(hdr), 1, f);
+            (void) fwrite(h, 64, tiles, f);
+            fclose(f);
+        }
+    }
+    free(h);
 }
 
 extern "C" int
@@ -298,9 +348,10 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.enc = c->tab->enc;
     a.n = n;
     a.mode = mode;
-    a.c = coord(c, tiles);
+    a.c = coord(c, tiles, st);
     uint32_t grid = (uint32_t) (tiles < c->enc_grid_max ? tiles : c->enc_grid_max);
     HIPCHK(c, launch_encode(a, grid, st));
+    dump_trace(c, 0, tiles, grid, st);
     return QHUFF_OK;
 }
 
@@ -331,10 +382,11 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.win = c->tab->win;
     a.sorted = c->tab->sorted;
     a.n = n;
-    a.c = coord(c, tiles);
+    a.c = coord(c, tiles, st);
     a.lp = c->lp;
     uint32_t grid = (uint32_t) (tiles < c->dec_grid_max ? tiles : c->dec_grid_max);
     HIPCHK(c, launch_decode(a, grid, st));
+    dump_trace(c, 1, tiles, grid, st);
     return QHUFF_OK;
 }
 
