@@ -102,7 +102,7 @@ int qhuff_decode_batch(qhuff_ctx *ctx, const uint8_t *in,
 /* Host-memory variants (PCIe-inclusive path: host -> pinned staging ->
  * device -> kernel -> device -> pinned -> host).  Synchronous.  in_off and
  * the returned out_off are host arrays of n + 1 entries; out must hold the
- * corresponding bound.  *out_total receives out_off[n]. */
+ * corresponding bound; out_off[n] is the output total. */
 int qhuff_encode_batch_host(qhuff_ctx *ctx, const uint8_t *in,
                             const uint32_t *in_off, uint32_t n, unsigned mode,
                             uint8_t *out, uint32_t *out_off);
@@ -159,6 +159,12 @@ const char *qhuff_last_error(qhuff_ctx *ctx);
  * (outputs of that launch are invalid).  Negative QHUFF_E* on HIP failure. */
 #define QHUFF_DEVERR_SPIN 1
 int qhuff_device_error(qhuff_ctx *ctx);
+
+/* Diagnostic: launch kernel `which` (0 encode, 1 decode) with `grid`
+ * workgroups in census mode and report in *resident how many of them were
+ * on the device at the same time.  Synchronous. */
+int qhuff_residency(qhuff_ctx *ctx, int which, uint32_t grid,
+                    uint32_t *resident);
 
 /* ---- multi-GPU sharding helpers (host arithmetic only) ----------------
  * Byte-balanced contiguous partition of a batch into g shards: writes

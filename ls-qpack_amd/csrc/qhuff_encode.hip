@@ -272,132 +272,184 @@ size_string(const EncArgs &a, const Src &src, uint32_t rs, uint32_t re,
     return z;
 }
 
-// the tile whose look-back / copy-out is deferred to the next iteration
+// the unit whose look-back / copy-out is deferred to the next iteration
 struct EncDeferred
 {
-    uint32_t tile, cnt, total, par;
+    uint32_t tile, lo, hi;     // strings [lo, hi) of `tile`
+    uint32_t total;            // output bytes of the unit
+    uint32_t unit_off;         // output bytes of the tile's earlier units
+    uint32_t par;              // stage parity holding its output
     uint32_t staged_out;
-    uintptr_t pa;              // input span (slow path)
-    uint32_t staged_in;
+    bool first, last;          // first / last unit of its tile
 };
 
-// store wave: look-back + copy-out + out_off of the deferred tile
+// look-back wave: the deferred unit's output base (see the decoder's
+// resolve_unit_base)
 __device__ __forceinline__ uint64_t
-enc_finish(const EncArgs &a, QH_LDS EncSmem *sm, const EncDeferred &df,
-           int64_t *known_tile, uint64_t *known_incl)
+enc_resolve_unit_base(const Coord &c, const EncDeferred &df, int64_t *known_tile,
+                      uint64_t *known_incl, uint64_t *tile_base)
 {
-    const int lane = threadIdx.x & 63;
-    const uint64_t base = (a.c.dbg & kDbgNoLookback) ? (uint64_t) df.tile << 16
-        : look_back_wave(a.c, df.tile, df.total, *known_tile, *known_incl);
-    *known_tile = df.tile;
-    *known_incl = base + df.total;
+    if (df.first)
+    {
+        uint32_t polls = 0;
+        stamp(c, df.tile, 11);
+        *tile_base = (c.dbg & kDbgNoLookback) ? (uint64_t) df.tile << 16
+            : look_back_wave(c, df.tile, df.total, *known_tile, *known_incl,
+                             &polls, df.last);
+        stamp(c, df.tile, 12);
+        stamp_value(c, df.tile, 14, polls);
+    }
+    const uint64_t ub = *tile_base + df.unit_off;
+    if (df.last)
+    {
+        if (!df.first && !(c.dbg & kDbgNoLookback) && (threadIdx.x & 63) == 0)
+            __hip_atomic_store(&c.flags[df.tile],
+                               kFlagInc | ((uint64_t) c.epoch << 40)
+                                        | ((ub + df.total) & kValMask),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *known_tile = df.tile;
+        *known_incl = ub + df.total;
+    }
+    return ub;
+}
+
+// every thread: copy-out and out_off of the deferred unit; a unit whose
+// output did not fit the stage is packed again by every lane straight to
+// global memory (input read from global)
+__device__ __forceinline__ void
+enc_finish(const EncArgs &a, QH_LDS EncSmem *sm, const EncDeferred &df,
+           uint64_t base)
+{
+    const int tid = threadIdx.x;
     if (a.c.dbg & kDbgNoStore)
-        return base;
-    const uint64_t s0 = (uint64_t) df.tile * kTile;
+        return;
+    const uint32_t ucnt = df.hi - df.lo;
+    const uint64_t s0 = (uint64_t) df.tile * kTile + df.lo;
     QH_GLB uint32_t *gout_off = glb(a.out_off);
     if (df.staged_out)
         copy_out(sm->out[df.par], a.out + base, df.total);
-    for (int t = lane; t < (int) df.cnt; t += 64)
-        gout_off[s0 + t] = (uint32_t) (base + sm->excl[df.par][t]);
-    if (df.tile == a.c.n_tiles - 1 && lane == 0)
+    else if (tid < (int) ucnt)
+    {
+        const QH_GLB uint32_t *gin_off = glb(a.in_off);
+        const uint32_t o0 = gin_off[s0 + tid], o1 = gin_off[s0 + tid + 1];
+        const uintptr_t pa = (uintptr_t) (a.in + o0) & ~(uintptr_t) 3;
+        const uint32_t rs = (uint32_t) ((uintptr_t) (a.in + o0) - pa);
+        const uint32_t re = rs + (o1 - o0);
+        EncGlb src{(const QH_GLB uint32_t *) pa};
+        EncSize z = size_string(a, src, rs, re, sm->len);
+        const uint32_t adj = (uint32_t) ((uintptr_t) a.out & 3);
+        Packer<PackGlb> pk;
+        pk.sink.out = a.out - adj;
+        const uint32_t p0 = adj + (uint32_t) base + sm->excl[df.par][tid];
+        pk.init(p0, p0 + z.size);
+        emit_string(src, rs, re, a.mode, z.huff, z.plen, sm->enc, pk);
+    }
+    if (tid < (int) ucnt)
+        gout_off[s0 + tid] = (uint32_t) (base + sm->excl[df.par][tid]);
+    if (df.last && df.tile == a.c.n_tiles - 1 && tid == 0)
         gout_off[a.n] = (uint32_t) (base + df.total);
-    return base;
+    stamp(a.c, df.tile, 13);
 }
 
-// slow path (tile output too large for the stage): every lane packs its
-// string again straight to global memory, input read from global
-__device__ __forceinline__ void
-enc_finish_slow(const EncArgs &a, QH_LDS EncSmem *sm, const EncDeferred &df,
-                uint64_t base)
-{
-    const int tid = threadIdx.x;
-    if ((a.c.dbg & kDbgNoStore) || tid >= (int) df.cnt)
-        return;
-    const QH_GLB uint32_t *gin_off = glb(a.in_off);
-    const uint64_t s0 = (uint64_t) df.tile * kTile;
-    const uint32_t o0 = gin_off[s0 + tid], o1 = gin_off[s0 + tid + 1];
-    const uintptr_t pa = (uintptr_t) (a.in + o0) & ~(uintptr_t) 3;
-    const uint32_t rs = (uint32_t) ((uintptr_t) (a.in + o0) - pa);
-    const uint32_t re = rs + (o1 - o0);
-    EncGlb src{(const QH_GLB uint32_t *) pa};
-    EncSize z = size_string(a, src, rs, re, sm->len);
-    const uint32_t adj = (uint32_t) ((uintptr_t) a.out & 3);
-    Packer<PackGlb> pk;
-    pk.sink.out = a.out - adj;
-    const uint32_t p0 = adj + (uint32_t) base + sm->excl[df.par][tid];
-    pk.init(p0, p0 + z.size);
-    emit_string(src, rs, re, a.mode, z.huff, z.plen, sm->enc, pk);
-}
-
-__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(3, 3))) void
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 3))) void
 qhuff_encode_kernel(EncArgs a)
 {
     __shared__ EncSmem smem;
     __shared__ uint64_t s_base;
+    __shared__ uint32_t s_claim;           // tile after `next` (look-back wave)
+    __shared__ uint32_t s_red;             // next unit's end (unit_vote)
+    __shared__ unsigned long long s_acc;   // tile aggregate accumulator
     QH_LDS EncSmem *sm = (QH_LDS EncSmem *) &smem;
+    QH_LDS uint32_t *red = (QH_LDS uint32_t *) &s_red;
     const int tid = threadIdx.x;
-    const bool ldw = !is_store_wave();
+    const bool lbw = is_lb_wave();
+    if (a.c.dbg & kDbgCensus)
+    {
+        census(a.c);
+        return;
+    }
 
     const QH_GLB u32x2 *genc = (const QH_GLB u32x2 *) a.enc;
-    const u32x2 e_t = genc[tid];
-    sm->enc[tid] = e_t;
-    sm->len[tid] = (uint8_t) e_t.y;
+    {
+        const u32x2 e_t = genc[tid];
+        sm->enc[tid] = e_t;
+        sm->len[tid] = (uint8_t) e_t.y;
+    }
     if (tid == 0)
+    {
         sm->enc[256] = genc[256];
+        s_acc = 0;
+        s_red = 1;
+    }
 
     const QH_GLB uint32_t *gin_off = glb(a.in_off);
-    const uint32_t G = gridDim.x;
-    uint32_t tile = blockIdx.x;
+    uint32_t tile, next;
+    claim_first(a.c, &tile, &next);
     if (tile >= a.c.n_tiles)
         return;
 
-    // prologue: offsets + input of the first tile (load waves)
+    // prologue: offsets, first unit and its input
     Prefetch<kEncChunks> pf;
     uint32_t cnt = (uint32_t) min((uint64_t) kTile, a.n - (uint64_t) tile * kTile);
-    if (ldw)
-    {
-        pf.load_offsets(gin_off, (uint64_t) tile * kTile, cnt);
-        pf.store_offsets(sm->off[0], cnt);
-    }
+    pf.load_offsets(gin_off, (uint64_t) tile * kTile, cnt);
+    pf.store_offsets(sm->off[0], cnt);
     __syncthreads();
-    Span sp0 = tile_span(a.in, sm->off[0], cnt, kEncInCapL);
+    unit_vote(a.in, sm->off[0], 0, cnt, kEncInCapL, red);
+    __syncthreads();
+    uint32_t lo = 0, hi = s_red;
+    Span sp0 = unit_span(a.in, sm->off[0], lo, hi, kEncInCapL);
     uintptr_t sp_pa = sp0.pa;
     uint32_t sp_n16 = sp0.n16;
     uint32_t sp_staged = sp0.staged;
-    if (sp_staged && ldw)
+    if (sp_staged)
     {
         pf.load_chunks(sp_pa, sp_n16);
         pf.store_chunks<false>((QH_LDS u32x4 *) sm->in, sp_n16);
     }
     uint32_t cur = 0, par = 0;
+    uint32_t unit_off = 0;
     int64_t known_tile = -1;
-    uint64_t known_incl = 0;
+    uint64_t known_incl = 0, tile_base = 0;
     bool pending = false;
-    EncDeferred df = {0, 0, 0, 0, 0, 0, 0};
+    EncDeferred df = {0, 0, 0, 0, 0, 0, 0, false, false};
 
     for (;;)
     {
         const QH_LDS uint32_t *off = sm->off[cur];
-        const uint32_t next = tile + G;
+        const bool last = hi == cnt;
         const bool has_next = next < a.c.n_tiles;
-        const uint32_t cnt_n = has_next
+        const bool more = !last || has_next;
+        const uint32_t lo_n = last ? 0 : hi;
+        const uint32_t cnt_n = !last ? cnt : has_next
             ? (uint32_t) min((uint64_t) kTile, a.n - (uint64_t) next * kTile) : 0;
+        uint32_t claimed = a.c.n_tiles;
+        if (tid == kBlock - 64 && last && has_next)
+            claimed = claim_tile(a.c, next);      // consumed after sizing
         if (threadIdx.x < 64)
         {
             stamp(a.c, tile, 0);
             stamp(a.c, tile, 1);
+            stamp_value(a.c, tile, 15, blockIdx.x);
+            stamp_value(a.c, tile, 8, ((uint64_t) lo << 32) | hi);
         }
-        if (has_next && ldw)
+        if (last && has_next)
             pf.load_offsets(gin_off, (uint64_t) next * kTile, cnt_n);
+        if (tid == 0)
+            s_red = lo_n + 1;
 
-        // 1. length sort + sizing (E1 / the framing choice of E3)
+        // 1. length sort + sizing (E1 / the framing choice of E3); each
+        //    wave adds its byte total to the tile aggregate at once
+        const uint32_t ucnt = hi - lo;
         uint32_t key = 0;
-        if (tid < (int) cnt)
-            key = min((off[tid + 1] - off[tid]) >> 1, (uint32_t) kBuckets - 1);
+        if (tid < (int) ucnt)
+            key = min((off[lo + tid + 1] - off[lo + tid]) >> 1,
+                      (uint32_t) kBuckets - 1);
         const uint32_t my = sort_by_bucket(key, sm->cnt, sm->perm);
-        const bool valid = my < cnt;
-        const uint32_t rs = valid ? (uint32_t) ((uintptr_t) (a.in + off[my]) - sp_pa) : 0;
-        const uint32_t re = valid ? (uint32_t) ((uintptr_t) (a.in + off[my + 1]) - sp_pa) : 0;
+
+        const bool valid = my < ucnt;
+        const uint32_t si = lo + (valid ? my : 0);
+        const uint32_t rs = valid ? (uint32_t) ((uintptr_t) (a.in + off[si]) - sp_pa) : 0;
+        const uint32_t re = valid ? (uint32_t) ((uintptr_t) (a.in + off[si + 1]) - sp_pa) : 0;
         EncSize z = {0, 0, true};
         if (valid)
         {
@@ -406,61 +458,66 @@ qhuff_encode_kernel(EncArgs a)
                                         rs, re, sm->len);
             sm->size[my] = z.size;
         }
+        publish_wave_total(a.c, tile, valid ? z.size : 0u, last,
+                           (QH_LDS unsigned long long *) &s_acc);
         if (threadIdx.x < 64)
             stamp(a.c, tile, 2);
-        else if (!ldw)
-            stamp(a.c, tile, 3);
-        if (has_next && ldw)
+
+        // look-back wave: the deferred unit's base
+        if (lbw)
+            stamp(a.c, tile, 5);
+        if (pending && lbw)
+        {
+            const uint64_t b = enc_resolve_unit_base(a.c, df, &known_tile,
+                                                     &known_incl, &tile_base);
+            if ((tid & 63) == 0)
+                s_base = b;
+        }
+        if (tid == kBlock - 64)
+            s_claim = claimed;
+        if (lbw)
+            stamp(a.c, tile, 6);
+        if (last && has_next)
             pf.store_offsets(sm->off[cur ^ 1], cnt_n);
         __syncthreads();
+        const uint32_t next2 = s_claim;
         if (threadIdx.x < 64)
             stamp(a.c, tile, 4);
+        const QH_LDS uint32_t *off_n = last ? sm->off[cur ^ 1] : off;
+        if (more)
+            unit_vote(a.in, off_n, lo_n, cnt_n, kEncInCapL, red);
 
-        // 2. scan in string order
-        const uint32_t sz_t = tid < (int) cnt ? sm->size[tid] : 0;
+        // 2. scan in string order, clear this parity's stage; next loads
+        const uint32_t sz_t = tid < (int) ucnt ? sm->size[tid] : 0;
         uint32_t total;
         const uint32_t ex_t = block_excl_scan(sz_t, &sm->scr, &total);
+        const uint32_t hi_n = s_red;
         sm->excl[par][tid] = ex_t;
         const bool staged_out = total + 64 <= (uint32_t) kEncOutCapL;
         if (staged_out)
         {
             QH_LDS u32x4 *o4 = (QH_LDS u32x4 *) sm->out[par];
             const uint32_t n16 = (total + 16 + 15) / 16 + 1;
-            for (uint32_t i = tid; i < n16; i += kTile)
+            for (uint32_t i = tid; i < n16; i += kBlock)
                 o4[i] = (u32x4){0, 0, 0, 0};
         }
-
-        // 3. load waves: next tile's input loads; store wave: deferred
-        //    tile's look-back + copy-out + offsets, then this aggregate
         uintptr_t nx_pa = 0;
         uint32_t nx_n16 = 0, nx_staged = 0;
-        if (has_next)
+        if (more)
         {
-            Span t = tile_span(a.in, sm->off[cur ^ 1], cnt_n, kEncInCapL);
+            Span t = unit_span(a.in, off_n, lo_n, hi_n, kEncInCapL);
             nx_pa = t.pa;
             nx_n16 = t.n16;
             nx_staged = t.staged;
-            if (nx_staged && ldw)
+            if (nx_staged)
                 pf.load_chunks(nx_pa, nx_n16);
         }
-        if (!ldw)
-            stamp(a.c, tile, 5);
-        if (pending && !ldw)
-        {
-            const uint64_t b = enc_finish(a, sm, df, &known_tile, &known_incl);
-            if ((tid & 63) == 0)
-                s_base = b;
-        }
-        if (!ldw)
-        {
-            publish_aggregate(a.c, tile, total);
-            stamp(a.c, tile, 6);
-        }
         __syncthreads();
-        if (pending && !df.staged_out)
-            enc_finish_slow(a, sm, df, s_base);
 
-        // 4. pack (E2 / E3) into the LDS output stage of this parity
+        // 3. the deferred unit leaves (other parity); pack (E2 / E3) this
+        //    unit into its parity of the stage
+        if (pending)
+            enc_finish(a, sm, df, s_base);
         const uint32_t myex = valid ? sm->excl[par][my] : 0;
         if (staged_out && valid && !(a.c.dbg & kDbgNoCodec))
         {
@@ -475,41 +532,52 @@ qhuff_encode_kernel(EncArgs a)
                             a.mode, z.huff, z.plen, sm->enc, pk);
         }
         df.tile = tile;
-        df.cnt = cnt;
+        df.lo = lo;
+        df.hi = hi;
         df.total = total;
+        df.unit_off = unit_off;
         df.par = par;
         df.staged_out = staged_out;
+        df.first = lo == 0;
+        df.last = last;
         pending = true;
+        unit_off = last ? 0 : unit_off + total;
         __syncthreads();
         if (threadIdx.x < 64)
             stamp(a.c, tile, 7);
-        if (!has_next)
+        if (!more)
             break;
-        if (nx_staged && ldw)
+        if (nx_staged)
             pf.store_chunks<false>((QH_LDS u32x4 *) sm->in, nx_n16);
-        tile = next;
-        cnt = cnt_n;
+        if (last)
+        {
+            tile = next;
+            next = next2;
+            cnt = cnt_n;
+            cur ^= 1;
+        }
+        lo = lo_n;
+        hi = hi_n;
         sp_pa = nx_pa;
         sp_n16 = nx_n16;
         sp_staged = nx_staged;
-        cur ^= 1;
         par ^= 1;
     }
-    if (!ldw)
+    if (lbw)
     {
-        const uint64_t b = enc_finish(a, sm, df, &known_tile, &known_incl);
+        const uint64_t b = enc_resolve_unit_base(a.c, df, &known_tile,
+                                                 &known_incl, &tile_base);
         if ((tid & 63) == 0)
             s_base = b;
     }
     __syncthreads();
-    if (!df.staged_out)
-        enc_finish_slow(a, sm, df, s_base);
+    enc_finish(a, sm, df, s_base);
 }
 
 hipError_t
 launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st)
 {
-    hipLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(kTile), 0, st, a);
+    hipLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(kBlock), 0, st, a);
     return hipGetLastError();
 }
 
@@ -518,7 +586,7 @@ encode_occupancy(int *blocks_per_cu)
 {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
         blocks_per_cu, reinterpret_cast<const void *>(qhuff_encode_kernel),
-        kTile, 0);
+        kBlock, 0);
 }
 
 size_t

@@ -34,7 +34,8 @@ struct qhuff_ctx
     DevTables *tab;                      // device
     LongParams lp;
     unsigned long long *flags;           // device, cap_tiles entries
-    uint32_t *err;                       // device error word
+    uint32_t *err;                       // device: [0] error word, [1..3]
+                                         // census, then claim counters
     uint64_t cap_tiles;
     uint32_t epoch;
     uint32_t dbg;                        // QHUFF_DEBUG ablation switches
@@ -48,6 +49,9 @@ struct qhuff_ctx
     size_t d_stage_cap;
     char err_msg[256];
 };
+
+// device words: [0] error, [1..3] census, then the claim counters
+constexpr size_t kErrWords = kCtrStride * (1 + 2 * kGroups);
 
 // blocks per CU that are certainly co-resident: the occupancy answer, no more
 // than the LDS allows at a 2 KiB allocation granule, and at least 1
@@ -143,9 +147,9 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     }
     e = hipMemcpy(c->tab, &dt, sizeof(dt), hipMemcpyHostToDevice);
     if (e == hipSuccess)
-        e = hipMalloc((void **) &c->err, sizeof(uint32_t));
+        e = hipMalloc((void **) &c->err, kErrWords * sizeof(uint32_t));
     if (e == hipSuccess)
-        e = hipMemset(c->err, 0, sizeof(uint32_t));
+        e = hipMemset(c->err, 0, kErrWords * sizeof(uint32_t));
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess)
@@ -257,8 +261,11 @@ prepare_launch(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
     c->epoch = (c->epoch + 1) & kEpochMask;
     if (c->epoch == 0)
     {
-        // wrapped: stale flags could alias the new epoch
+        // wrapped: stale flags could alias the new epoch, and the claim
+        // counter of epoch 1 was last used, not cleared
         HIPCHK(c, hipMemsetAsync(c->flags, 0, c->cap_tiles * 8, st));
+        HIPCHK(c, hipMemsetAsync(c->err + kCtrStride, 0,
+                                 2 * kGroups * kCtrStride * sizeof(uint32_t), st));
         c->epoch = 1;
     }
     return QHUFF_OK;
@@ -271,49 +278,82 @@ coord(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
     k.trace = nullptr;
     if (c->trace_path)
     {
-        if (c->trace_cap < 8 * tiles)
+        if (c->trace_cap < kTraceSlots * tiles)
         {
             if (c->trace)
                 (void) hipFree(c->trace);
             c->trace = nullptr;
             c->trace_cap = 0;
-            if (hipMalloc((void **) &c->trace, 64 * tiles) == hipSuccess)
-                c->trace_cap = 8 * tiles;
+            if (hipMalloc((void **) &c->trace, 8 * kTraceSlots * tiles) == hipSuccess)
+                c->trace_cap = kTraceSlots * tiles;
         }
         if (c->trace)
         {
-            (void) hipMemsetAsync(c->trace, 0, 64 * tiles, st);
+            (void) hipMemsetAsync(c->trace, 0, 8 * kTraceSlots * tiles, st);
             k.trace = c->trace;
         }
     }
     k.flags = c->flags;
     k.err = c->err;
+    k.ctr = c->err + kCtrStride;
     k.epoch = c->epoch;
     k.n_tiles = (uint32_t) tiles;
     k.dbg = c->dbg;
     return k;
 }
 
+extern "C" int
+qhuff_residency(qhuff_ctx *c, int which, uint32_t grid, uint32_t *resident)
+{
+    if (!c || !resident || grid == 0 || (which != 0 && which != 1))
+        return QHUFF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = c->own_stream;
+    HIPCHK(c, hipMemsetAsync(c->err + 1, 0, 3 * sizeof(uint32_t), st));
+    Coord k = coord(c, grid, st);
+    k.dbg = kDbgCensus;
+    k.trace = nullptr;
+    if (which == 0)
+    {
+        EncArgs a = {};
+        a.c = k;
+        HIPCHK(c, launch_encode(a, grid, st));
+    }
+    else
+    {
+        DecArgs a = {};
+        a.c = k;
+        HIPCHK(c, launch_decode(a, grid, st));
+    }
+    HIPCHK(c, hipStreamSynchronize(st));
+    uint32_t v[2] = {0, 0};
+    HIPCHK(c, hipMemcpy(v, c->err + 1, sizeof(v), hipMemcpyDeviceToHost));
+    *resident = v[1];
+    return QHUFF_OK;
+}
+
 // diagnostic only (QHUFF_TRACE=path): synchronises, appends one record
-// {u32 'QTRC', kind, tiles, grid, tiles * 8 u64 stamps} to the file
+// {u32 'QTR2', kind, tiles, grid, slots, tiles * slots u64 stamps}
 static void
 dump_trace(qhuff_ctx *c, uint32_t kind, uint64_t tiles, uint32_t grid,
            hipStream_t st)
 {
-    if (!c->trace || c->trace_cap < 8 * tiles)
+    const size_t bytes = 8 * kTraceSlots * tiles;
+    if (!c->trace || c->trace_cap < kTraceSlots * tiles)
         return;
-    unsigned long long *h = (unsigned long long *) malloc(64 * tiles);
+    unsigned long long *h = (unsigned long long *) malloc(bytes);
     if (!h)
         return;
-    if (hipMemcpyAsync(h, c->trace, 64 * tiles, hipMemcpyDeviceToHost, st) == hipSuccess
+    if (hipMemcpyAsync(h, c->trace, bytes, hipMemcpyDeviceToHost, st) == hipSuccess
             && hipStreamSynchronize(st) == hipSuccess)
     {
         FILE *f = fopen(c->trace_path, "ab");
         if (f)
         {
-            const uint32_t hdr[4] = {0x43525451u, kind, (uint32_t) tiles, grid};
+            const uint32_t hdr[5] = {0x32525451u, kind, (uint32_t) tiles, grid,
+                                     (uint32_t) kTraceSlots};
             (void) fwrite(hdr, sizeof(hdr), 1, f);
-            (void) fwrite(h, 64, tiles, f);
+            (void) fwrite(h, 8 * kTraceSlots, tiles, f);
             fclose(f);
         }
     }

@@ -24,8 +24,10 @@ constexpr int kWinBits = 12;
 constexpr int kWinSize = 1 << kWinBits;
 constexpr int kMaxLong = 16;            // lengths 13..30 that occur (14 used)
 
-// window entry: sym0 [7:0] | sym1 [15:8] | len0 [19:16] | lensum [23:20] |
-//               nsym [25:24]; nsym == 0: first code is longer than 12 bits
+// window entry: sym0 [7:0] | sym1 [15:8] | bits consumed by all nsym
+//               symbols c [19:16] | len0 [23:20] | nsym [25:24] |
+//               32 - c [31:26] (the decoder's alignbit shift); nsym == 0:
+//               the first code is longer than 12 bits (entry < 1 << 24)
 struct LongLen { uint32_t len, first, count, base; };
 
 struct HostTables

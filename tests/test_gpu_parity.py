@@ -227,6 +227,25 @@ def test_decode_garbage(codec):
     assert st.sum() > 1000 and (st == 0).sum() > 1000
 
 
+@pytest.mark.parametrize("lo,hi", [(30, 90), (100, 400), (0, 2000)])
+def test_multi_unit_tiles(codec, lo, hi):
+    """Tiles whose input overflows the LDS stage are coded as several units
+    by one workgroup (and single strings past the stage read from global):
+    every mode, both directions, mixed with ordinary tiles."""
+    rng = random.Random(lo * 7 + hi)
+    strs = (rand_strings(rng, 3000, ALPHAS["token"], lo, hi)
+            + rand_strings(rng, 2000, ALPHAS["token"], 8, 64)
+            + rand_strings(rng, 1000, ALPHAS["long"], lo, hi))
+    rng.shuffle(strs)
+    data, off = pack(strs)
+    for mode in (0, 7):
+        check_encode(codec, data, off, mode)
+    h, ho = O.encode_batch(data, off, 0)
+    out, oo, st = check_decode(codec, h, ho)
+    assert not st.any() and np.array_equal(out, data)
+    assert codec.device_error() == 0
+
+
 def test_edge_batches(codec):
     # n = 0
     for mode in (0, 7):

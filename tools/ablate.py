@@ -50,9 +50,11 @@ def main():
             if it >= 5:
                 te.append(e0.elapsed_time(e1) * 1e3)
                 td.append(e1.elapsed_time(e2) * 1e3)
+        err = c.device_error()
         c.close()
         res[v] = (float(np.median(te)), float(np.median(td)))
-        print("dbg=%2d  enc %8.1f us   dec %8.1f us" % (v, *res[v]), flush=True)
+        print("dbg=%#5x  enc %8.1f us   dec %8.1f us  device_error %d"
+              % (v, *res[v], err), flush=True)
     os.environ.pop("QHUFF_DEBUG", None)
     print(json.dumps({str(k): v for k, v in res.items()}))
 

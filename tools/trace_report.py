@@ -7,6 +7,8 @@ Slots per tile (see qhuff_device.h stamp()):
   2 wave 0 codec done                      3 store wave codec done
   4 wave 0 past barrier 1                  5 store wave: finish starts
   6 store wave: finish + publish done      7 wave 0 past the last barrier
+  11-13 (in the finished tile's own record) look-back start, look-back
+  done, copy-out done; 14 look-back re-polls; 15 workgroup
 Diagnostic only: tracing synchronises after every launch."""
 import os
 import struct
@@ -24,13 +26,13 @@ def read(path):
     with open(path, "rb") as f:
         b = f.read()
     p = 0
-    while p + 16 <= len(b):
-        magic, kind, tiles, grid = struct.unpack_from("<4I", b, p)
-        assert magic == 0x43525451
-        p += 16
-        st = np.frombuffer(b, dtype=np.uint64, count=8 * tiles, offset=p)
-        p += 64 * tiles
-        recs.append((kind, tiles, grid, st.reshape(tiles, 8).astype(np.int64)))
+    while p + 20 <= len(b):
+        magic, kind, tiles, grid, slots = struct.unpack_from("<5I", b, p)
+        assert magic == 0x32525451
+        p += 20
+        st = np.frombuffer(b, dtype=np.uint64, count=slots * tiles, offset=p)
+        p += 8 * slots * tiles
+        recs.append((kind, tiles, grid, st.reshape(tiles, slots).astype(np.int64)))
     return recs
 
 
@@ -38,12 +40,14 @@ def report(kind, tiles, grid, s):
     name = "enc" if kind == 0 else "dec"
     rt = s[:, 0]
     span_us = (rt.max() - rt.min()) / 100.0
-    # clock from consecutive iterations of one workgroup
-    t = np.arange(tiles)
-    nxt = t + grid
-    ok = nxt < tiles
-    dmt = s[nxt[ok], 1] - s[t[ok], 1]
-    drt = s[nxt[ok], 0] - s[t[ok], 0]
+    # consecutive iterations of one workgroup (slot 15 = workgroup)
+    order = np.lexsort((rt, s[:, 15]))
+    wg = s[order, 15]
+    same = wg[1:] == wg[:-1]
+    t = order[:-1][same]
+    nx = order[1:][same]
+    dmt = s[nx, 1] - s[t, 1]
+    drt = s[nx, 0] - s[t, 0]
     clk = np.median(dmt / np.maximum(drt, 1)) * 100e6
     cyc = lambda x: x / clk * 1e6                     # cycles -> us
     ph = {
@@ -53,11 +57,12 @@ def report(kind, tiles, grid, s):
         "finish+publish (store)": s[:, 6] - s[:, 5],
         "store wave idle before finish": s[:, 5] - s[:, 3],
         "w0 after barrier1 -> end": s[:, 7] - s[:, 4],
-        "iteration total": np.concatenate([dmt, [0]])[:0],
+        "look-back (own record)": s[:, 12] - s[:, 11],
+        "copy-out+offsets (own record)": s[:, 13] - s[:, 12],
     }
     print("%s: tiles %d grid %d  first-start..last-start %.1f us  clock %.2f GHz"
           % (name, tiles, grid, span_us, clk / 1e9))
-    first = rt[:grid]
+    first = np.array([rt[s[:, 15] == w].min() for w in np.unique(s[:, 15])])
     print("   launch ramp (first-iteration start spread): %.2f us"
           % ((first.max() - first.min()) / 100.0))
     for k, v in ph.items():
@@ -68,8 +73,12 @@ def report(kind, tiles, grid, s):
               % (k, v.mean(), np.median(v), np.percentile(v, 90), v.max()))
     it = cyc(dmt.astype(np.float64))
     print("   %-32s mean %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us"
-          % ("iteration (t -> t+G)", it.mean(), np.median(it),
+          % ("iteration (same workgroup)", it.mean(), np.median(it),
              np.percentile(it, 90), it.max()))
+    polls = s[:, 14]
+    print("   look-back polls: mean %.2f  p90 %d  max %d  (>1 poll: %.1f%% of tiles)"
+          % (polls.mean(), np.percentile(polls, 90), polls.max(),
+             100.0 * (polls > 0).mean()))
     # iteration count per WG
     per_wg = (tiles + grid - 1) // grid
     print("   iterations per WG: %d..%d" % (tiles // grid, per_wg))
@@ -83,7 +92,7 @@ def main():
         import torch
         import qhuff
         n = int(os.environ.get("N", 1 << 20))
-        data, off = qhuff.synth_batch(n)
+        data, off = qhuff.synth_batch(n, max_len=int(os.environ.get("MAXLEN", 64)))
         dev = torch.device("cuda", 0)
         d = torch.from_numpy(data).to(dev)
         o = torch.from_numpy(off.view(np.int32)).to(dev)
