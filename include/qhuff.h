@@ -160,11 +160,10 @@ const char *qhuff_last_error(qhuff_ctx *ctx);
 #define QHUFF_DEVERR_SPIN 1
 int qhuff_device_error(qhuff_ctx *ctx);
 
-/* Diagnostic: launch kernel `which` (0 encode, 1 decode) with `grid`
- * workgroups in census mode and report in *resident how many of them were
- * on the device at the same time.  Synchronous. */
-int qhuff_residency(qhuff_ctx *ctx, int which, uint32_t grid,
-                    uint32_t *resident);
+/* Diagnostic: synchronise and copy the context's kDbgClock per-phase cycle
+ * sums (QHUFF_DEBUG=0x40 launches) into out[0..n) (n <= 8), then clear
+ * them.  Returns QHUFF_OK or a negative QHUFF_E* code. */
+int qhuff_debug_clock(qhuff_ctx *ctx, uint64_t *out, uint32_t n);
 
 /* ---- multi-GPU sharding helpers (host arithmetic only) ----------------
  * Byte-balanced contiguous partition of a batch into g shards: writes

@@ -8,48 +8,46 @@
 //      the last complete symbol are >= 8 or not all ones
 //      (lsqpack.c:5362-5426, 3482-3497)
 //
-// One string per lane.  The tile's input is staged in LDS as big-endian
-// dwords; each lane keeps a 64-bit bit buffer in registers, refilled from
-// the stage one aligned dword at a time (the refill read is independent of
-// the table lookup, so one LDS round trip sits on the per-step dependency
-// chain).  A step looks the top 12 bits up in a window table (up to two
-// symbols of <= 12 bits); codes of 13..30 bits take a canonical length
-// search behind a wave-uniform branch.  While >= 32 real bits remain the
-// step needs no padding or tail logic; the last < 32 bits run a careful
-// epilogue that pads with ones (as huff_decode_fast pads its last window,
+// One string per lane, one 64-string tile per wave (qhuff_device.h).  The
+// tile's input is staged in the wave's LDS region as big-endian dwords;
+// each lane keeps a 64-bit bit buffer in registers, refilled from the stage
+// one aligned dword at a time (the refill read is independent of the table
+// lookup, so one LDS round trip sits on the per-step dependency chain).  A
+// step looks the top 12 bits up in a window table (up to two symbols of
+// <= 12 bits); codes of 13..30 bits take a canonical length search behind a
+// wave-uniform branch.  While >= 32 real bits remain the step needs no
+// padding or tail logic; the last < 32 bits run a careful epilogue that
+// pads with ones (as huff_decode_fast pads its last window,
 // lsqpack.c:5364-5365) and applies the D3 rule.
 //
 // Output bytes land in a byte-granular per-string arena slot.  After the
-// workgroup scan the slots are compacted into an LDS output stage; the
-// tile's look-back and copy-out are deferred to the workgroup's next
-// iteration, when every predecessor has long published its aggregate
-// (persistent grid, static tile assignment t = blockIdx.x + k * gridDim.x).
+// wave scan of the sizes they are compacted into the (now dead) input stage
+// and copied out with 16-byte stores once the look-back has resolved the
+// tile's output base.
 #include "qhuff_kernels.h"
 
 namespace qhuff {
 
-constexpr int kDecInCap = 7680;                        // staged input bytes
-constexpr int kDecOutCap = 10 * 1024;                  // staged output bytes
+constexpr int kDecWaves = 16;                          // waves per workgroup
+constexpr int kDecInCap = 3072;                        // staged input bytes
 // byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
 // most 8/5 of its input, plus one byte written past the end by the
 // two-byte emitter
-constexpr int kArenaBytes = 2 * kTile + 8 * kDecInCap / 5 + 16;
+constexpr int kArenaBytes = 2 * kWT + 8 * kDecInCap / 5 + 32;
+constexpr int kDecChunks = kDecInCap / 16 / 64;        // 16-B chunks per lane
+constexpr int kDecOutChunks = 3;                       // covers a stage of 3072 B
+
+struct DecWave                       // one wave's private LDS region
+{
+    alignas(16) uint32_t in[kDecInCap / 4];   // BE input dwords; output stage
+    alignas(16) uint8_t arena[kArenaBytes];
+};
 
 struct DecSmem
 {
     uint32_t win[kWinSize];
     uint16_t sorted[257];
-    LongLen longc[kMaxLong];         // canonical long-code params
-    uint32_t off[2][kTile + 1];      // current / next tile offsets
-    uint32_t size[kTile];            // bit 31: rejected string
-    uint32_t excl_p[kTile];          // tile offsets of the deferred tile
-    uint32_t cnt[kBuckets];
-    uint16_t perm[kTile];
-    uint8_t stat_p[kTile];           // status of the deferred tile
-    LdsScratch scr;
-    alignas(16) uint32_t in[kDecInCap / 4 + 8];        // big-endian dwords
-    alignas(16) uint32_t out[(kDecOutCap + 64) / 4];   // 16 B pad in front
-    alignas(16) uint8_t arena[kArenaBytes];
+    DecWave w[kDecWaves];
 };
 
 struct DecLds                        // big-endian dwords staged in LDS
@@ -77,25 +75,28 @@ struct DecGlb                        // raw little-endian bytes in global
     }
 };
 
-// long-code step: canonical search over code lengths 13..30 (uniform table,
-// unrolled selects)
+// long-code step: canonical search over the code lengths 13..30 (compile-
+// time parameters, one compare-and-select per length)
+template <int I>
+__device__ __forceinline__ void
+long_search(uint32_t w, uint32_t &L, uint32_t &idx)
+{
+    if constexpr (I < (int) kLongTab.n)
+    {
+        constexpr LongLen ll = kLongTab.l[I];
+        const uint32_t off = (w >> (32 - ll.len)) - ll.first;
+        const bool hit = (L == 0) & (off < ll.count);
+        L = hit ? ll.len : L;
+        idx = hit ? ll.base + off : idx;
+        long_search<I + 1>(w, L, idx);
+    }
+}
+
 __device__ __forceinline__ uint32_t
-long_code(uint32_t w, const QH_LDS LongLen *lc, const QH_LDS uint16_t *s_sorted,
-          uint32_t *len)
+long_code(uint32_t w, const QH_LDS uint16_t *s_sorted, uint32_t *len)
 {
     uint32_t L = 0, idx = 0;
-#pragma unroll
-    for (int i = 0; i < kMaxLong; ++i)
-    {
-        // lengths past lp.n are padded with count 0 (never hit); uniform
-        // LDS addresses (broadcast reads)
-        const u32x4 ll = ((const QH_LDS u32x4 *) lc)[i];   // len first count base
-        uint32_t v = w >> (32 - ll.x);
-        uint32_t off = v - ll.y;
-        bool hit = (L == 0) & (off < ll.z);
-        L = hit ? ll.x : L;
-        idx = hit ? ll.w + off : idx;
-    }
+    long_search<0>(w, L, idx);
     *len = L;
     return s_sorted[idx];
 }
@@ -109,7 +110,7 @@ template <bool GATED, class Emit>
 __device__ __forceinline__ bool
 main_step(bool act, uint32_t d, uint32_t &hi, uint32_t &lo, uint32_t &bits,
           uint32_t &rem, uint32_t &p, const QH_LDS uint32_t *s_win,
-          const QH_LDS uint16_t *s_sorted, const QH_LDS LongLen *lp, Emit &emit)
+          const QH_LDS uint16_t *s_sorted, Emit &emit)
 {
     uint32_t e = s_win[hi >> (32 - kWinBits)];
     bool ok = true;
@@ -117,7 +118,7 @@ main_step(bool act, uint32_t d, uint32_t &hi, uint32_t &lo, uint32_t &bits,
     {
         // a code of 13..30 bits: synthesize the entry of a one-symbol step
         uint32_t L;
-        const uint32_t sym = long_code(hi, lp, s_sorted, &L);
+        const uint32_t sym = long_code(hi, s_sorted, &L);
         const bool lng = (GATED ? act : true) & (e < (1u << 24));
         ok = !(lng & (sym == 256));
         const uint32_t el = (sym & 0xff) | (L << 16) | (1u << 24)
@@ -155,7 +156,7 @@ template <class Src, class Emit>
 __device__ __forceinline__ int
 decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
               const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
-              const QH_LDS LongLen *lp, Emit &emit)
+              Emit &emit)
 {
     uint32_t rem = bitend - bit0;            // real bits not yet consumed
     uint32_t hi = 0, lo = 0, bits = 0, p = 0;
@@ -178,7 +179,7 @@ decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
     {
         const uint32_t d = src.dw_ahead(p, bitend);
         const bool ok = main_step<false>(true, d, hi, lo, bits, rem, p, s_win,
-                                         s_sorted, lp, emit);
+                                         s_sorted, emit);
         bad |= !ok;
         rem = ok ? rem : 0u;                 // leave phase 1 (rare)
     } while (!__builtin_amdgcn_ballot_w64(rem < 32));
@@ -188,7 +189,7 @@ decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
     {
         const uint32_t d = src.dw_ahead(p, bitend);
         const bool ok = main_step<true>(act, d, hi, lo, bits, rem, p, s_win,
-                                        s_sorted, lp, emit);
+                                        s_sorted, emit);
         bad |= !ok;
         act = act & ok & (rem >= 32);
     } while (__builtin_amdgcn_ballot_w64(act));
@@ -209,7 +210,7 @@ decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
         if (__builtin_amdgcn_ballot_w64(!fin & (ns == 0) & (rem > kWinBits)))
         {
             uint32_t L;
-            const uint32_t sym = long_code(w, lp, s_sorted, &L);
+            const uint32_t sym = long_code(w, s_sorted, &L);
             const bool lng = (ns == 0) & (rem > kWinBits);
             c = lng ? L : c;
             val = lng ? sym : val;
@@ -271,347 +272,198 @@ struct GlobalEmit                            // slow path: byte stores
     }
 };
 
-constexpr int kDecChunks = (kDecInCap / 16 + kLoadThreads - 1) / kLoadThreads;
-
-// the unit whose look-back / copy-out is deferred to the next iteration
-struct Deferred
+// per-lane string bounds of a tile relative to its span
+struct LaneStr
 {
-    uint32_t tile, lo, hi;     // strings [lo, hi) of `tile`
-    uint32_t total;            // output bytes of the unit
-    uint32_t unit_off;         // output bytes of the tile's earlier units
-    uint32_t staged_out;       // output sits in sm->out (else re-decode)
-    bool first, last;          // first / last unit of its tile
+    bool valid;
+    uint32_t rs, re;                 // byte positions relative to span.pa
+    uint32_t slot0;                  // arena slot
 };
 
-// look-back wave: the deferred unit's output base.  The first unit of a
-// tile resolves the tile's base by look-back; the last one publishes the
-// tile's inclusive prefix (a one-unit tile does both in look_back_wave).
-__device__ __forceinline__ uint64_t
-resolve_unit_base(const Coord &c, const Deferred &df, int64_t *known_tile,
-                  uint64_t *known_incl, uint64_t *tile_base)
+__device__ __forceinline__ LaneStr
+lane_str(const uint8_t *in, const TileOffs &to, uint32_t cnt, const Span &sp)
 {
-    if (df.first)
-    {
-        uint32_t polls = 0;
-        stamp(c, df.tile, 11);
-        *tile_base = (c.dbg & kDbgNoLookback) ? (uint64_t) df.tile << 16
-            : look_back_wave(c, df.tile, df.total, *known_tile, *known_incl,
-                             &polls, df.last);
-        stamp(c, df.tile, 12);
-        stamp_value(c, df.tile, 14, polls);
-    }
-    const uint64_t ub = *tile_base + df.unit_off;
-    if (df.last)
-    {
-        if (!df.first && !(c.dbg & kDbgNoLookback) && (threadIdx.x & 63) == 0)
-            __hip_atomic_store(&c.flags[df.tile],
-                               kFlagInc | ((uint64_t) c.epoch << 40)
-                                        | ((ub + df.total) & kValMask),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *known_tile = df.tile;
-        *known_incl = ub + df.total;
-    }
-    return ub;
+    LaneStr ls;
+    const uint32_t lane = lane_id();
+    ls.valid = lane < cnt;
+    const uint32_t A = to.first();
+    ls.rs = ls.valid ? (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa) : 0;
+    ls.re = ls.valid ? (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa) : 0;
+    ls.slot0 = 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
+    return ls;
 }
 
-// every thread: copy-out, offsets and status of the deferred unit; a unit
-// whose output did not fit the LDS stage is decoded again by every lane
-// straight to global memory (input read from global)
+// arena slot -> stage at byte D (wave-synchronous; other lanes write the
+// neighbouring bytes): bytes up to a dword boundary, whole dwords, tail
 __device__ __forceinline__ void
-finish_unit(const DecArgs &a, QH_LDS DecSmem *sm, const Deferred &df,
-            uint64_t base)
+compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
 {
-    const int tid = threadIdx.x;
-    if (a.c.dbg & kDbgNoStore)
-        return;
-    const uint32_t ucnt = df.hi - df.lo;
-    const uint64_t s0 = (uint64_t) df.tile * kTile + df.lo;
-    QH_GLB uint32_t *gout_off = glb(a.out_off);
-    QH_GLB uint8_t *gstat = glb(a.status);
-    if (df.staged_out)
-        copy_out(sm->out, a.out + base, df.total);
-    else if (tid < (int) ucnt && sm->stat_p[tid] == QHUFF_DEC_OK)
-    {
-        const QH_GLB uint32_t *gin_off = glb(a.in_off);
-        const uint32_t o0 = gin_off[s0 + tid], o1 = gin_off[s0 + tid + 1];
-        const uintptr_t pa = (uintptr_t) (a.in + o0) & ~(uintptr_t) 3;
-        const uint32_t rs = (uint32_t) ((uintptr_t) (a.in + o0) - pa);
-        GlobalEmit em{a.out + base + sm->excl_p[tid], 0};
-        decode_string(DecGlb{(const QH_GLB uint32_t *) pa}, 8 * rs,
-                      8 * (rs + o1 - o0), sm->win, sm->sorted, sm->longc, em);
-    }
-    if (tid < (int) ucnt)
-    {
-        gout_off[s0 + tid] = (uint32_t) (base + sm->excl_p[tid]);
-        gstat[s0 + tid] = sm->stat_p[tid];
-    }
-    if (df.last && df.tile == a.c.n_tiles - 1 && tid == 0)
-        gout_off[a.n] = (uint32_t) (base + df.total);
-    stamp(a.c, df.tile, 13);
+    uint32_t h = (4 - ((uint32_t) (uintptr_t) dstb & 3)) & 3;
+    h = h < n ? h : n;
+    for (uint32_t i = 0; i < h; ++i)
+        dstb[i] = src[i];
+    const QH_LDS uint8_t *s2 = src + h;
+    const uint32_t s3 = (uint32_t) ((uintptr_t) s2 & 3);
+    const QH_LDS uint32_t *sw = (const QH_LDS uint32_t *) (s2 - s3);
+    QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
+    const uint32_t nb = (n - h) >> 2;
+    for (uint32_t k = 0; k < nb; ++k)
+        dw[k] = align_bytes(sw[k + 1], sw[k], s3);
+    for (uint32_t i = h + 4 * nb; i < n; ++i)
+        dstb[i] = src[i];
 }
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 3))) void
+__global__ __launch_bounds__(64 * kDecWaves) void
 qhuff_decode_kernel(DecArgs a)
 {
     __shared__ DecSmem smem;
-    __shared__ uint64_t s_base;
-    __shared__ uint32_t s_claim;           // tile after `next` (look-back wave)
-    __shared__ uint32_t s_red;             // next unit's end (unit_vote)
-    __shared__ unsigned long long s_acc;   // tile aggregate accumulator
     QH_LDS DecSmem *sm = (QH_LDS DecSmem *) &smem;
-    QH_LDS uint32_t *red = (QH_LDS uint32_t *) &s_red;
     const int tid = threadIdx.x;
-    const bool lbw = is_lb_wave();
-    if (a.c.dbg & kDbgCensus)
-    {
-        census(a.c);
-        return;
-    }
     {
         const QH_GLB u32x4 *gw = (const QH_GLB u32x4 *) glb(a.win);
         QH_LDS u32x4 *sw = (QH_LDS u32x4 *) sm->win;
-        for (int i = tid; i < kWinSize / 4; i += kBlock)
+        for (int i = tid; i < kWinSize / 4; i += 64 * kDecWaves)
             sw[i] = gw[i];
         const QH_GLB uint16_t *gs = glb(a.sorted);
-        sm->sorted[tid] = gs[tid];
-        if (tid == 0)
-        {
-            sm->sorted[256] = gs[256];
-            s_acc = 0;
-            s_red = 1;
-        }
-        if (tid < 4 * kMaxLong)
-            ((QH_LDS uint32_t *) sm->longc)[tid] =
-                ((const uint32_t *) a.lp.l)[tid];
+        if (tid < 257)
+            sm->sorted[tid] = gs[tid];
+        clear_next_launch(a.c);
     }
+    __syncthreads();                 // the only workgroup barrier
+
+    const uint32_t lane = lane_id();
+    QH_LDS DecWave *wv = &sm->w[tid >> 6];
+    QH_LDS uint32_t *stage = wv->in;
     const QH_GLB uint32_t *gin_off = glb(a.in_off);
-    uint32_t tile, next;
-    claim_first(a.c, &tile, &next);
-    if (tile >= a.c.n_tiles)
-        return;
+    QH_GLB uint32_t *gout_off = glb(a.out_off);
+    QH_GLB uint8_t *gstat = glb(a.status);
+    const uint32_t n_waves = gridDim.x * kDecWaves;
+    const uint32_t gid = wave_gid(kDecWaves);
+    const uint32_t nt = a.c.n_tiles;
+    const uint32_t dbg = a.c.dbg;
 
-    // prologue: offsets, first unit and its input
-    Prefetch<kDecChunks> pf;
-    uint32_t cnt = (uint32_t) min((uint64_t) kTile, a.n - (uint64_t) tile * kTile);
-    pf.load_offsets(gin_off, (uint64_t) tile * kTile, cnt);
-    pf.store_offsets(sm->off[0], cnt);
-    __syncthreads();
-    unit_vote(a.in, sm->off[0], 0, cnt, kDecInCap, red);
-    __syncthreads();
-    uint32_t lo = 0, hi = s_red;
-    Span sp0 = unit_span(a.in, sm->off[0], lo, hi, kDecInCap);
-    uintptr_t sp_pa = sp0.pa;
-    uint32_t sp_n16 = sp0.n16;
-    uint32_t sp_staged = sp0.staged;
-    if (sp_staged)
-    {
-        pf.load_chunks(sp_pa, sp_n16);
-        pf.store_chunks<true>((QH_LDS u32x4 *) sm->in, sp_n16);
-    }
-    uint32_t cur = 0;
-    uint32_t unit_off = 0;                        // bytes of earlier units
-    int64_t known_tile = -1;                      // see look_back_wave()
-    uint64_t known_incl = 0, tile_base = 0;
-    bool pending = false;
-    Deferred df = {0, 0, 0, 0, 0, 0, false, false};
+    auto tile_cnt = [&](uint32_t t) -> uint32_t {
+        return (uint32_t) min((uint64_t) kWT, a.n - (uint64_t) t * kWT);
+    };
 
+    // Tiles are claimed just in time: a wave claims its next tile only when
+    // it is about to code it, so claim order is processing order and a
+    // look-back only ever waits on tiles whose codec is already running.
+    // The claim -> offsets -> input latency of one wave hides under the
+    // codec work of the other waves on its SIMD.
+    PhaseClock clk;
+    clk.init(dbg);
     for (;;)
     {
-        const QH_LDS uint32_t *off = sm->off[cur];
-        const bool last = hi == cnt;              // this unit ends the tile
-        const bool has_next = next < a.c.n_tiles;
-        const bool more = !last || has_next;      // a next unit exists
-        const uint32_t lo_n = last ? 0 : hi;
-        const uint32_t cnt_n = !last ? cnt : has_next
-            ? (uint32_t) min((uint64_t) kTile, a.n - (uint64_t) next * kTile) : 0;
-        uint32_t claimed = a.c.n_tiles;
-        if (tid == kBlock - 64 && last && has_next)
-            claimed = claim_tile(a.c, next);      // consumed after the codec
-        if (threadIdx.x < 64)
+        const uint32_t t = claim_tile(a.c, gid, n_waves);
+        clk.lap(0);
+        if (t >= nt)
+            break;
+        const uint32_t cnt = tile_cnt(t);
+        TileOffs to;
+        to.load(gin_off, (uint64_t) t * kWT, cnt);
+        const Span sp = tile_span(a.in, to.first(), to.last(), kDecInCap);
+        if (sp.staged)
         {
-            stamp(a.c, tile, 0);
-            stamp(a.c, tile, 1);
-            stamp_value(a.c, tile, 15, blockIdx.x);
-            stamp_value(a.c, tile, 8, ((uint64_t) lo << 32) | hi);
+            Chunks<kDecChunks> ch;
+            ch.load(sp);
+            ch.store<true>((QH_LDS u32x4 *) stage, sp.n16);
         }
-        if (last && has_next)
-            pf.load_offsets(gin_off, (uint64_t) next * kTile, cnt_n);
-        if (tid == 0)
-            s_red = lo_n + 1;
+        wave_sync();
+        clk.lap(1);
 
-        // 1. sort + decode the unit into the arena; each wave adds its byte
-        //    total to the tile aggregate as soon as its strings are done
-        const uint32_t ucnt = hi - lo;
-        uint32_t key = 0;
-        if (tid < (int) ucnt)
-            key = min((off[lo + tid + 1] - off[lo + tid]) >> 1,
-                      (uint32_t) kBuckets - 1);
-        const uint32_t my = sort_by_bucket(key, sm->cnt, sm->perm);
-
-        const bool valid = my < ucnt;
-        const uint32_t A = off[lo];
-        const uint32_t si = lo + (valid ? my : 0);
-        const uint32_t rs = valid ? (uint32_t) ((uintptr_t) (a.in + off[si]) - sp_pa) : 0;
-        const uint32_t re = valid ? (uint32_t) ((uintptr_t) (a.in + off[si + 1]) - sp_pa) : 0;
-        const uint32_t slot0 = 2 * my + (uint32_t) ((8ull * (off[si] - A)) / 5);
-        uint32_t mine = 0;
-        if (valid)
+        // 1. decode this tile (input staged in LDS, or read from global)
+        const LaneStr ls = lane_str(a.in, to, cnt, sp);
+        int r = 0;
+        if (ls.valid)
         {
-            int r;
-            if (a.c.dbg & kDbgNoCodec)
-                r = (int) (re - rs);
-            else if (sp_staged)
+            if (dbg & kDbgNoCodec)
+                r = (int) (ls.re - ls.rs);
+            else if (sp.staged)
             {
-                ArenaEmit em{sm->arena + slot0, 0};
-                r = decode_string(DecLds{sm->in}, 8 * rs, 8 * re, sm->win,
-                                  sm->sorted, sm->longc, em);
+                ArenaEmit em{wv->arena + ls.slot0, 0};
+                r = decode_string(DecLds{stage}, 8 * ls.rs, 8 * ls.re, sm->win,
+                                  sm->sorted, em);
             }
             else
             {
                 CountEmit em{0};
-                r = decode_string(DecGlb{(const QH_GLB uint32_t *) sp_pa},
-                                  8 * rs, 8 * re, sm->win, sm->sorted,
-                                  sm->longc, em);
+                r = decode_string(DecGlb{(const QH_GLB uint32_t *) sp.pa},
+                                  8 * ls.rs, 8 * ls.re, sm->win, sm->sorted,
+                                  em);
             }
-            sm->size[my] = r < 0 ? 0x80000000u : (uint32_t) r;
-            mine = r < 0 ? 0u : (uint32_t) r;
         }
-        publish_wave_total(a.c, tile, mine, last,
-                           (QH_LDS unsigned long long *) &s_acc);
-        if (threadIdx.x < 64)
-            stamp(a.c, tile, 2);
-        else if (lbw)
-            stamp(a.c, tile, 3);
+        const uint32_t sz = r < 0 ? 0u : (uint32_t) r;
+        const uint32_t incl = wave_incl_scan(sz);
+        const uint32_t excl = incl - sz;
+        clk.lap(2);
+        const uint32_t total = read_lane(incl, 63);
 
-        // look-back wave (shortest strings): the deferred unit's base
-        if (lbw)
-            stamp(a.c, tile, 5);
-        if (pending && lbw)
-        {
-            const uint64_t b = resolve_unit_base(a.c, df, &known_tile,
-                                                 &known_incl, &tile_base);
-            if ((tid & 63) == 0)
-                s_base = b;
-        }
-        if (tid == kBlock - 64)
-            s_claim = claimed;
-        if (lbw)
-            stamp(a.c, tile, 6);
-        if (last && has_next)
-            pf.store_offsets(sm->off[cur ^ 1], cnt_n);
-        __syncthreads();
-        const uint32_t next2 = s_claim;
-        if (threadIdx.x < 64)
-            stamp(a.c, tile, 4);
-        const QH_LDS uint32_t *off_n = last ? sm->off[cur ^ 1] : off;
-        if (more)
-            unit_vote(a.in, off_n, lo_n, cnt_n, kDecInCap, red);
+        // 2. publish the aggregate, issue the first look-back poll
+        LookBack lb;
+        if (!(dbg & kDbgNoLookback))
+            lb.start(a.c, t, total);
+        clk.lap(3);
 
-        // 2. the deferred unit leaves: copy-out, offsets, status
-        if (pending)
-            finish_unit(a, sm, df, s_base);
+        // 3. compaction: arena slots -> the (dead) input stage
+        const bool staged_out = sp.staged && total + 64 <= (uint32_t) kDecInCap;
+        wave_sync();
+        if (staged_out && sz && !(dbg & kDbgNoCodec))
+            compact_string(wv->arena + ls.slot0,
+                           (QH_LDS uint8_t *) stage + 16 + excl, sz);
+        wave_sync();
 
-        // 3. scan of this unit (its barrier also orders the copy-out reads
-        //    above before the stage is cleared below, and the votes before
-        //    the next unit's end is read); next unit's loads
-        const uint32_t szw_t = tid < (int) ucnt ? sm->size[tid] : 0;
-        const uint32_t sz_t = szw_t & 0x7fffffffu;
-        uint32_t total;
-        const uint32_t ex_t = block_excl_scan(sz_t, &sm->scr, &total);
-        const uint32_t hi_n = s_red;
-        uintptr_t nx_pa = 0;
-        uint32_t nx_n16 = 0, nx_staged = 0;
-        if (more)
-        {
-            Span t = unit_span(a.in, off_n, lo_n, hi_n, kDecInCap);
-            nx_pa = t.pa;
-            nx_n16 = t.n16;
-            nx_staged = t.staged;
-            if (nx_staged)
-                pf.load_chunks(nx_pa, nx_n16);
-        }
+        clk.lap(4);
 
-        // 4. compaction of this unit: arena slots -> output stage
-        const bool staged_out = sp_staged && total + 64 <= (uint32_t) kDecOutCap;
+        // 4. output base
+        const uint64_t base = (dbg & kDbgNoLookback) ? (uint64_t) t << 13
+                            : lb.finish(a.c);
+        clk.lap(5);
+
+        // 5. copy-out (stage -> registers -> 16-byte stores)
+        CopyOut<kDecOutChunks> co;
         if (staged_out)
+            co.gather(stage, a.out + base, total);
+        if (!(dbg & kDbgNoStore))
         {
-            QH_LDS u32x4 *o4 = (QH_LDS u32x4 *) sm->out;
-            const uint32_t n16 = (total + 16 + 15) / 16 + 1;
-            for (uint32_t i = tid; i < n16; i += kBlock)
-                o4[i] = (u32x4){0, 0, 0, 0};
-        }
-        sm->excl_p[tid] = ex_t;
-        sm->stat_p[tid] = (szw_t >> 31) ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
-        __syncthreads();
-        const uint32_t nout = valid ? sm->size[my] & 0x7fffffffu : 0;
-        if (staged_out && nout && !(a.c.dbg & kDbgNoCodec))
-        {
-            const uint32_t D = 16 + sm->excl_p[my];
-            const uint32_t dsh = 8 * (D & 3);
-            const QH_LDS uint8_t *src = sm->arena + slot0;
-            const uint32_t s3 = (uint32_t) ((uintptr_t) src & 3);
-            const QH_LDS uint32_t *sw = (const QH_LDS uint32_t *) (src - s3);
-            QH_LDS uint32_t *o = sm->out + (D >> 2);
-            const uint32_t nwd = (nout + 3) >> 2;
-            for (uint32_t k = 0; k < nwd; ++k)
+            if (staged_out)
+                co.store();
+            else if (sz && sp.staged)
             {
-                uint32_t w = align_bytes(sw[k + 1], sw[k], s3);
-                const uint32_t vb = nout - 4 * k;
-                if (vb < 4)
-                    w &= (1u << (8 * vb)) - 1;
-                __hip_atomic_fetch_or(&o[k], w << dsh, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (dsh)
-                    __hip_atomic_fetch_or(&o[k + 1], w >> (32 - dsh),
-                                          __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                // output larger than the stage: arena -> global, bytes
+                const QH_LDS uint8_t *src = wv->arena + ls.slot0;
+                QH_GLB uint8_t *dst = (QH_GLB uint8_t *) (a.out + base + excl);
+                for (uint32_t i = 0; i < sz; ++i)
+                    dst[i] = src[i];
             }
+            else if (sz && !(dbg & kDbgNoCodec))
+            {
+                // input larger than the stage: decode again, to global
+                GlobalEmit em{a.out + base + excl, 0};
+                decode_string(DecGlb{(const QH_GLB uint32_t *) sp.pa},
+                              8 * ls.rs, 8 * ls.re, sm->win, sm->sorted,
+                              em);
+            }
+            const uint64_t s0 = (uint64_t) t * kWT;
+            if (ls.valid)
+            {
+                gout_off[s0 + lane] = (uint32_t) (base + excl);
+                gstat[s0 + lane] = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+            }
+            if (t == nt - 1 && lane == 0)
+                gout_off[a.n] = (uint32_t) (base + total);
         }
-        df.tile = tile;
-        df.lo = lo;
-        df.hi = hi;
-        df.total = total;
-        df.unit_off = unit_off;
-        df.staged_out = staged_out;
-        df.first = lo == 0;
-        df.last = last;
-        pending = true;
-        unit_off = last ? 0 : unit_off + total;
-        __syncthreads();
-        if (threadIdx.x < 64)
-            stamp(a.c, tile, 7);
-        if (!more)
-            break;
-        if (nx_staged)
-            pf.store_chunks<true>((QH_LDS u32x4 *) sm->in, nx_n16);
-        if (last)
-        {
-            tile = next;
-            next = next2;
-            cnt = cnt_n;
-            cur ^= 1;
-        }
-        lo = lo_n;
-        hi = hi_n;
-        sp_pa = nx_pa;
-        sp_n16 = nx_n16;
-        sp_staged = nx_staged;
+        wave_sync();
+        clk.lap(6);
     }
-    if (lbw)
-    {
-        const uint64_t b = resolve_unit_base(a.c, df, &known_tile, &known_incl,
-                                             &tile_base);
-        if ((tid & 63) == 0)
-            s_base = b;
-    }
-    __syncthreads();
-    finish_unit(a, sm, df, s_base);
+    clk.flush(a.c.err);
 }
 
 hipError_t
 launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st)
 {
-    hipLaunchKernelGGL(qhuff_decode_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL(qhuff_decode_kernel, dim3(grid), dim3(64 * kDecWaves),
+                       0, st, a);
     return hipGetLastError();
 }
 
@@ -620,7 +472,13 @@ decode_occupancy(int *blocks_per_cu)
 {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
         blocks_per_cu, reinterpret_cast<const void *>(qhuff_decode_kernel),
-        kBlock, 0);
+        64 * kDecWaves, 0);
+}
+
+int
+decode_waves_per_block()
+{
+    return kDecWaves;
 }
 
 size_t

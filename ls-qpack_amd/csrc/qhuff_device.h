@@ -1,14 +1,22 @@
 // qhuff_device.h -- device-side building blocks shared by the encode and
-// decode tile kernels (gfx950, wave64, 256-thread workgroups).
+// decode kernels (gfx950, wave64).
+//
+// Execution model ("wave tiles"): a workgroup only exists to share one copy
+// of the static code tables in LDS.  After the single table-load barrier
+// every wave is an independent worker with a private LDS region; it claims
+// tiles of kWT = 64 strings (one string per lane), stages the tile's packed
+// input, runs the per-lane codec, scans the 64 output sizes with cross-lane
+// operations, resolves the tile's output base with a decoupled look-back
+// over per-tile flags, and copies the compacted output out with 16-byte
+// stores.  No workgroup barrier is ever taken inside the tile loop, so the
+// latency of one wave's loads / look-back polls hides under the codec work
+// of the other waves on its SIMD.
 //
 //   * explicit LDS / global address spaces (a generic pointer into LDS
 //     compiles to flat_load with global-memory latency)
-//   * workgroup exclusive scan
-//   * length-bucket counting sort of a tile's strings, so that each wave runs
-//     strings of similar length (the per-lane codec loops run as long as the
-//     wave's longest string)
-//   * 256-wide decoupled look-back over per-tile flags, with bounded spins
-//   * shifted, 16-byte-aligned copy-out of an LDS output stage
+//   * wave scans, wave-level decoupled look-back with bounded spins
+//   * grouped dynamic tile claims (no residency assumption)
+//   * split copy-out: stage -> registers, then 16-byte aligned stores
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -21,75 +29,62 @@ namespace qhuff {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kTile = 256;                  // strings per tile = threads per WG
-constexpr int kBuckets = 64;                // length buckets for the tile sort
+constexpr int kWT = 64;                     // strings per wave tile
 
-// look-back flag word: [63:62] state, [61:40] epoch, [39:0] byte count
-constexpr uint64_t kFlagAgg = 1ull << 62;
-constexpr uint64_t kFlagInc = 2ull << 62;
+// Look-back flag word: [63:42] launch epoch, [41:40] state (1 aggregate,
+// 2 inclusive), [39:0] byte count.  Epoch on top: within a launch an
+// inclusive flag compares above an aggregate one, and any flag of this
+// launch above every stale one, so super-tile flags published by different
+// waves use atomic max and are never downgraded.
+constexpr uint64_t kFlagAgg = 1ull << 40;
+constexpr uint64_t kFlagInc = 2ull << 40;
 constexpr uint64_t kValMask = (1ull << 40) - 1;
 constexpr uint32_t kEpochMask = (1u << 22) - 1;
 constexpr uint32_t kSpinLimit = 1u << 21;   // polls before giving up (~1 s)
+constexpr int kSuper = 64;                  // tiles per super tile
+// super-tile accumulator word: [63:48] tiles arrived, [47:0] byte sum
+constexpr uint64_t kAccOne = 1ull << 48;
+constexpr uint64_t kAccMask = kAccOne - 1;
 
 // ablation switches (timing experiments only; outputs are wrong when set)
-constexpr uint32_t kDbgNoLookback = 2;      // base = tile * 64 KiB
+constexpr uint32_t kDbgNoLookback = 2;      // base = tile * 8 KiB
 constexpr uint32_t kDbgNoStore = 4;         // skip the global output stores
 constexpr uint32_t kDbgNoCodec = 8;         // skip the per-string codec loops
-constexpr uint32_t kDbgCensus = 0x100;      // residency census only (below)
-constexpr uint32_t kDbgStatic = 0x200;      // static tile order (needs the
-                                            // whole grid resident)
+
+constexpr uint32_t kDbgClock = 0x40;        // per-phase cycle sums (below)
 
 // error bits reported through Coord::err
 constexpr uint32_t kErrSpin = 1;            // look-back spin limit hit
 
+// Dynamic tile order.  Waves form kGroups groups (global wave id mod
+// kGroups); group g owns tiles g, g + NG, g + 2 NG, ... (NG = min(kGroups,
+// waves)) and its waves claim them in order from the group's counter.  A
+// tile is only ever claimed by a running wave, and every wave processes its
+// claimed tiles in increasing order, so the lowest unfinished tile always
+// makes progress: the look-back needs no residency guarantee.  Spreading the
+// claims over kGroups counters keeps same-address atomics from serialising.
+// Launch `epoch` uses counter set epoch & 1 and clears the other set for the
+// next launch on the stream (a context's launches are stream-ordered).
+constexpr uint32_t kGroups = 64;
+constexpr uint32_t kCtrStride = 64;         // u32 per counter: 256 B apart
+
 struct Coord
 {
     unsigned long long *flags;              // per-tile look-back flags
+    unsigned long long *sflags;             // per-super-tile flags
+    unsigned long long *sacc;               // super accumulators [2][cap_super]
     uint32_t *err;                          // sticky device error word
     uint32_t *ctr;                          // claim counters [2][kGroups], strided
     uint32_t epoch;                         // launch tag carried in flags
     uint32_t n_tiles;
+    uint32_t cap_super;                     // sacc entries per parity
     uint32_t dbg;
-    unsigned long long *trace;              // QHUFF_TRACE: kTraceSlots per tile
 };
 
-constexpr int kTraceSlots = 16;
-
-// phase stamps for tools/trace_report.py (null trace: one scalar branch)
-__device__ __forceinline__ void
-stamp(const Coord &c, uint32_t tile, int slot)
+__device__ __forceinline__ uint32_t
+lane_id()
 {
-    if (c.trace && (threadIdx.x & 63) == 0)
-        c.trace[(uint64_t) kTraceSlots * tile + slot] =
-            slot == 0 ? __builtin_amdgcn_s_memrealtime()
-                      : __builtin_amdgcn_s_memtime();
-}
-
-__device__ __forceinline__ void
-stamp_value(const Coord &c, uint32_t tile, int slot, uint64_t v)
-{
-    if (c.trace && (threadIdx.x & 63) == 0)
-        c.trace[(uint64_t) kTraceSlots * tile + slot] = v;
-}
-
-struct LdsScratch                           // per-WG scan scratch
-{
-    uint32_t wsum[4];
-};
-
-// A workgroup is four waves, one string per lane (kBlock == kTile).  Every
-// wave decodes/encodes; wave 3 (the "look-back wave") also claims tiles and
-// resolves the decoupled look-back.  Tile aggregates are published by
-// whichever wave finishes its strings last (publish_wave_total), so a
-// tile's aggregate never waits for any look-back -- look-back waits cannot
-// chain from one workgroup to the next.  Copy-out of the deferred tile is
-// shared by all four waves.
-constexpr int kBlock = kTile;
-constexpr int kLoadThreads = kTile;
-__device__ __forceinline__ bool
-is_lb_wave()
-{
-    return threadIdx.x >= kTile - 64;
+    return threadIdx.x & 63;
 }
 
 __device__ __forceinline__ uint32_t
@@ -105,197 +100,194 @@ align_bytes(uint32_t hi, uint32_t lo, uint32_t sh)
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
-// workgroup exclusive scan of one uint32 per thread; *total = sum
 __device__ __forceinline__ uint32_t
-block_excl_scan(uint32_t v, QH_LDS LdsScratch *scr, uint32_t *total)
+uniform(uint32_t v)
 {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ uint32_t
+read_lane(uint32_t v, uint32_t lane)
+{
+    return __builtin_amdgcn_readlane(v, lane);
+}
+
+// orders this wave's LDS accesses across lanes (LDS instructions of one
+// wave execute in issue order; this stops the compiler moving them)
+__device__ __forceinline__ void
+wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// wave inclusive scan of one uint32 per lane
+__device__ __forceinline__ uint32_t
+wave_incl_scan(uint32_t v)
+{
+    const uint32_t lane = lane_id();
     uint32_t x = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1)
     {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d)
-            x += y;
+        const uint32_t y = __shfl_up(x, d, 64);
+        x += lane >= (uint32_t) d ? y : 0u;
     }
-    if (lane == 63)
-        scr->wsum[wave] = x;
-    __syncthreads();
-    uint32_t w0 = scr->wsum[0], w1 = scr->wsum[1], w2 = scr->wsum[2],
-             w3 = scr->wsum[3];
-    uint32_t before = (wave > 0 ? w0 : 0) + (wave > 1 ? w1 : 0)
-                    + (wave > 2 ? w2 : 0);
-    *total = w0 + w1 + w2 + w3;
-    return before + x - v;
+    return x;
 }
 
-// Counting sort of the tile's strings by length bucket (0..kBuckets-1).
-// Returns the tile-local string index this thread should process.  Waves
-// take 64-string runs of the sorted order; the look-back wave (wave 3),
-// which also resolves the look-back, takes the shortest run.
+template <class T>
+__device__ __forceinline__ T
+wave_sum(T v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1)
+        v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Per-phase cycle accounting (kDbgClock): each wave sums s_memtime deltas
+// per phase in registers and adds them once, at exit, to err[16 + 2 * ph]
+// (u64 pairs).  Phase list: see the kernels.
+constexpr int kPhases = 8;
+struct PhaseClock
+{
+    uint64_t t0;
+    uint64_t sum[kPhases];
+    bool on;
+
+    __device__ __forceinline__ void init(uint32_t dbg)
+    {
+        on = (dbg & kDbgClock) != 0;
+        for (int i = 0; i < kPhases; ++i)
+            sum[i] = 0;
+        t0 = on ? __builtin_amdgcn_s_memtime() : 0;
+    }
+    __device__ __forceinline__ void lap(int ph)
+    {
+        if (on)
+        {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            sum[ph] += t - t0;
+            t0 = t;
+        }
+    }
+    __device__ __forceinline__ void flush(uint32_t *err) const
+    {
+        if (on && (threadIdx.x & 63) == 0)
+            for (int i = 0; i < kPhases; ++i)
+                atomicAdd((unsigned long long *) (err + 16 + 2 * i),
+                          (unsigned long long) sum[i]);
+    }
+};
+
+// ---- tile claims -------------------------------------------------------
+
 __device__ __forceinline__ uint32_t
-sort_by_bucket(uint32_t key, QH_LDS uint32_t *s_cnt, QH_LDS uint16_t *s_perm)
+wave_gid(int waves_per_block)
 {
-    const int tid = threadIdx.x, lane = tid & 63;
-    if (tid < kBuckets)
-        s_cnt[tid] = 0;
-    __syncthreads();
-    const uint32_t pos = __hip_atomic_fetch_add(&s_cnt[key], 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-    __syncthreads();
-    if (tid < 64)
-    {
-        const uint32_t a = s_cnt[lane];
-        uint32_t x = a;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1)
-        {
-            uint32_t y = __shfl_up(x, d, 64);
-            if (lane >= d)
-                x += y;
-        }
-        s_cnt[lane] = x - a;
-    }
-    __syncthreads();
-    s_perm[s_cnt[key] + pos] = (uint16_t) tid;
-    __syncthreads();
-    return s_perm[(tid + 64) & (kTile - 1)];
+    return blockIdx.x * (uint32_t) waves_per_block + (threadIdx.x >> 6);
 }
 
-// Look-back by ONE wave (the look-back wave):
-// kLbK flags per lane, kLbWin predecessors per poll.  Position q of the
-// window (q = 64k + lane) is tile j - q.
-constexpr int kLbK = 12;
-constexpr int kLbWin = kLbK * 64;
-
-// known_tile / known_incl: a predecessor whose inclusive prefix the calling
-// workgroup already knows (its own previous tile), or known_tile = -1.  With
-// gridDim.x <= kLbWin one poll always reaches it.  Returns the exclusive
-// byte prefix of `tile` and publishes its inclusive value (lane 0).
-__device__ __forceinline__ uint64_t
-look_back_wave(const Coord &c, uint32_t tile, uint64_t agg,
-               int64_t known_tile, uint64_t known_incl, uint32_t *polls = nullptr,
-               bool publish = true)
+// lane 0 claims; the returned tile id is wave-uniform (n_tiles = none)
+__device__ __forceinline__ uint32_t
+claim_tile(const Coord &c, uint32_t gid, uint32_t n_waves)
 {
-    const int lane = threadIdx.x & 63;
-    const uint64_t ep = (uint64_t) c.epoch << 40;
-    uint64_t excl = 0;
-    int64_t j = (int64_t) tile - 1;
-    uint32_t spins = 0;
-    while (j >= 0)
-    {
-        uint64_t f[kLbK];
-#pragma unroll
-        for (int k = 0; k < kLbK; ++k)
-        {
-            const int64_t idx = j - lane - 64 * k;
-            if (idx < 0)
-                f[k] = kFlagInc | ep;                    // before tile 0
-            else if (idx == known_tile)
-                f[k] = kFlagInc | ep | (known_incl & kValMask);
-            else
-                f[k] = __hip_atomic_load(&c.flags[idx], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-        }
-        int F = kLbWin;                  // nearest inclusive position
-        uint64_t inv[kLbK];
-#pragma unroll
-        for (int k = kLbK - 1; k >= 0; --k)
-        {
-            const bool valid = ((f[k] >> 40) & kEpochMask) == c.epoch
-                             && (f[k] >> 62) != 0;
-            const bool inc = valid && (f[k] >> 62) == 2;
-            const uint64_t im = __ballot(inc);
-            inv[k] = __ballot(!valid);
-            if (im)
-                F = 64 * k + __builtin_ctzll(im);
-        }
-        const int fcap = F < kLbWin ? F : kLbWin - 1;
-        bool bad = false;
-#pragma unroll
-        for (int k = 0; k < kLbK; ++k)
-        {
-            const int lim = fcap - 64 * k;
-            const uint64_t m = lim >= 63 ? ~0ull
-                             : (lim < 0 ? 0ull : ((2ull << lim) - 1));
-            bad |= (inv[k] & m) != 0;
-        }
-        if (bad)
-        {
-            if (++spins > ((c.dbg & kDbgStatic) ? (1u << 12) : kSpinLimit))
-            {
-                if (lane == 0)
-                    atomicOr(c.err, kErrSpin);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        uint64_t mine = 0;
-#pragma unroll
-        for (int k = 0; k < kLbK; ++k)
-            mine += (lane + 64 * k <= F) ? (f[k] & kValMask) : 0;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1)
-            mine += __shfl_xor(mine, d, 64);
-        excl += mine;
-        if (F < kLbWin)
-            break;
-        j -= kLbWin;
-    }
-    if (lane == 0 && publish)
-        __hip_atomic_store(&c.flags[tile],
-                           kFlagInc | ep | ((excl + agg) & kValMask),
+    const uint32_t ng = n_waves < kGroups ? n_waves : kGroups;
+    const uint32_t g = gid % ng;
+    uint32_t k = 0;
+    if (lane_id() == 0)
+        k = __hip_atomic_fetch_add(
+            &c.ctr[((c.epoch & 1) * kGroups + g) * kCtrStride], 1u,
+            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    k = uniform(k);
+    const uint64_t t = g + (uint64_t) k * ng;
+    return t < c.n_tiles ? (uint32_t) t : c.n_tiles;
+}
+
+// clears the claim counters and super accumulators of the next launch on
+// the stream (they use the other parity; every thread of the grid helps)
+__device__ __forceinline__ void
+clear_next_launch(const Coord &c)
+{
+    const uint32_t par = (c.epoch + 1) & 1;
+    if (blockIdx.x == 0 && threadIdx.x < kGroups)
+        __hip_atomic_store(&c.ctr[(par * kGroups + threadIdx.x) * kCtrStride],
+                           0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // all of them: the next launch may hold more tiles than this one
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < c.cap_super;
+         i += gridDim.x * blockDim.x)
+        __hip_atomic_store(&c.sacc[(uint64_t) par * c.cap_super + i], 0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (polls)
-        *polls = spins;
-    return excl;
 }
 
-// Next-tile prefetch: offsets and up to NCH 16-byte input chunks per thread
-// held in registers while the current tile is processed.
-template <int NCH>
-struct Prefetch
+// ---- tile offsets ------------------------------------------------------
+
+// Lane i holds the start offset of string i of the tile and of string i+1
+// (clamped to the tile end).  `cnt` strings, cnt in [1, 64].
+struct TileOffs
 {
-    uint32_t off0, off1;            // two offsets per load thread (257 needed)
+    uint32_t o0, o1;
+
+    __device__ __forceinline__ void load(const QH_GLB uint32_t *in_off,
+                                         uint64_t s0, uint32_t cnt)
+    {
+        const uint32_t lane = lane_id();
+        o0 = in_off[s0 + (lane < cnt ? lane : cnt)];
+        o1 = in_off[s0 + (lane + 1 < cnt ? lane + 1 : cnt)];
+    }
+    __device__ __forceinline__ uint32_t first() const { return read_lane(o0, 0); }
+    __device__ __forceinline__ uint32_t last() const { return read_lane(o1, 63); }
+};
+
+// A tile's input span [pa, pb) rounded out to 16-byte boundaries.
+struct Span
+{
+    uintptr_t pa;
+    uint32_t n16;
+    bool staged;
+};
+
+__device__ __forceinline__ Span
+tile_span(const uint8_t *in, uint32_t A, uint32_t B, uint32_t cap)
+{
+    Span sp;
+    const uintptr_t a = (uintptr_t) (in + A);
+    const uintptr_t b = (uintptr_t) (in + B);
+    sp.pa = a & ~(uintptr_t) 15;
+    const uintptr_t pb = (b + 15) & ~(uintptr_t) 15;
+    sp.n16 = (uint32_t) ((pb - sp.pa) >> 4);
+    sp.staged = pb - sp.pa <= (uintptr_t) cap;
+    return sp;
+}
+
+// A tile's staged input held in registers between its load and its LDS
+// write: NCH 16-byte chunks per lane.
+template <int NCH>
+struct Chunks
+{
     u32x4 ch[NCH];
 
-    __device__ __forceinline__ void load_offsets(const QH_GLB uint32_t *in_off,
-                                                 uint64_t s0, uint32_t cnt)
+    __device__ __forceinline__ void load(const Span &sp)
     {
-        const int tid = threadIdx.x;       // load waves only
-        off0 = tid <= (int) cnt ? in_off[s0 + tid] : 0;
-        const int t1 = tid + kLoadThreads;
-        off1 = t1 <= (int) cnt ? in_off[s0 + t1] : 0;
-    }
-    __device__ __forceinline__ void store_offsets(QH_LDS uint32_t *s_off,
-                                                  uint32_t cnt) const
-    {
-        const int tid = threadIdx.x;
-        if (tid <= (int) cnt)
-            s_off[tid] = off0;
-        const int t1 = tid + kLoadThreads;
-        if (t1 <= (int) cnt)
-            s_off[t1] = off1;
-    }
-    __device__ __forceinline__ void load_chunks(uintptr_t pa, uint32_t n16)
-    {
+        const uint32_t lane = lane_id();
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
         {
-            uint32_t i = threadIdx.x + k * kLoadThreads;
-            if (i < n16)
-                ch[k] = ((const QH_GLB u32x4 *) pa)[i];
+            const uint32_t i = lane + 64u * k;
+            if (i < sp.n16)
+                ch[k] = ((const QH_GLB u32x4 *) sp.pa)[i];
         }
     }
     template <bool SWAP>
-    __device__ __forceinline__ void store_chunks(QH_LDS u32x4 *dst,
-                                                 uint32_t n16) const
+    __device__ __forceinline__ void store(QH_LDS u32x4 *dst, uint32_t n16) const
     {
+        const uint32_t lane = lane_id();
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
         {
-            uint32_t i = threadIdx.x + k * kLoadThreads;
+            const uint32_t i = lane + 64u * k;
             if (i < n16)
             {
                 u32x4 v = ch[k];
@@ -308,213 +300,243 @@ struct Prefetch
     }
 };
 
-// A tile's input span [pa, pb) rounded out to 16-byte boundaries.
-struct Span
+// ---- two-level decoupled look-back, one wave per tile ---------------------
+//
+// With thousands of waves each holding one tile, a flat look-back has to
+// walk back through ~one tile per running wave before it meets an inclusive
+// flag.  Tiles are therefore grouped into super tiles of kSuper consecutive
+// tiles.  After its codec a tile publishes its aggregate and adds it to its
+// super tile's accumulator; the tile whose add completes the count publishes
+// the super tile's aggregate.  A tile's exclusive prefix is then
+//   (aggregates of the earlier tiles of its super tile, back to an
+//    inclusive one if there is one)
+// + (super aggregates back to an inclusive super flag),
+// one 64-wide window of each, polled together.  Only aggregates are waited
+// for, and those are published right after codecs that are already running
+// (tiles are claimed in order), so no wait chains through other look-backs.
+// The last tile of a super tile publishes the super tile's inclusive flag.
+
+__device__ __forceinline__ bool
+flag_valid(uint64_t f, uint32_t epoch)
 {
-    uintptr_t pa;
-    uint32_t n16;
-    bool staged;
+    return (f >> 42) == epoch && ((f >> 40) & 3) != 0;
+}
+
+__device__ __forceinline__ bool
+flag_inc(uint64_t f)
+{
+    return ((f >> 40) & 3) == 2;
+}
+
+struct LookBack
+{
+    uint32_t tile, s;
+    uint64_t total;
+    uint64_t acc_old;            // returned by the super accumulator add (lane 0)
+    uint64_t ft, fs;             // polled tile / super flags (one per lane)
+
+    __device__ __forceinline__ uint64_t ep(const Coord &c) const
+    {
+        return (uint64_t) c.epoch << 42;
+    }
+    __device__ __forceinline__ void poll_tiles(const Coord &c)
+    {
+        const uint32_t lane = lane_id();
+        const uint32_t f0 = s * kSuper;
+        ft = (tile - f0 > lane) ? __hip_atomic_load(&c.flags[tile - 1 - lane],
+                                                    __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                : 0ull;
+    }
+    // super flags s-1-lane-64*back (before super 0: inclusive 0)
+    __device__ __forceinline__ uint64_t poll_supers(const Coord &c,
+                                                    uint32_t back) const
+    {
+        const int64_t j = (int64_t) s - 1 - lane_id() - 64 * (int64_t) back;
+        return j < 0 ? (kFlagInc | ep(c))
+                     : __hip_atomic_load(&c.sflags[j], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    // publish the aggregate, add to the super accumulator, issue the polls
+    __device__ __forceinline__ void start(const Coord &c, uint32_t t,
+                                          uint64_t tot)
+    {
+        tile = t;
+        s = t / kSuper;
+        total = tot;
+        acc_old = 0;
+        if (lane_id() == 0)
+        {
+            __hip_atomic_store(&c.flags[t], kFlagAgg | ep(c) | (tot & kValMask),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            acc_old = __hip_atomic_fetch_add(
+                &c.sacc[(uint64_t) (c.epoch & 1) * c.cap_super + s],
+                kAccOne + tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        poll_tiles(c);
+        fs = poll_supers(c, 0);
+    }
+
+    __device__ __forceinline__ void publish_super(const Coord &c, uint64_t state,
+                                                  uint64_t v) const
+    {
+        if (lane_id() == 0)
+            __hip_atomic_fetch_max(&c.sflags[s], state | ep(c) | (v & kValMask),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    __device__ __forceinline__ bool spin(const Coord &c, uint32_t *spins) const
+    {
+        if (++*spins > kSpinLimit)
+        {
+            if (lane_id() == 0)
+                atomicOr(c.err, kErrSpin);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        return true;
+    }
+
+    // returns the exclusive prefix of the tile; publishes its inclusive one
+    __device__ __forceinline__ uint64_t finish(const Coord &c)
+    {
+        const uint32_t lane = lane_id();
+        const uint32_t f0 = s * kSuper;
+        const uint32_t in_super = c.n_tiles - f0 < (uint32_t) kSuper
+                                ? c.n_tiles - f0 : (uint32_t) kSuper;
+        // the add that completes the super tile publishes its aggregate
+        const uint64_t old = ((uint64_t) read_lane((uint32_t) (acc_old >> 32), 0) << 32)
+                           | read_lane((uint32_t) acc_old, 0);
+        if ((old >> 48) == in_super - 1)
+            publish_super(c, kFlagAgg, (old + total) & kAccMask);
+
+        uint32_t spins = 0;
+        uint64_t excl = 0;
+        const uint32_t nq = tile - f0;               // earlier tiles in super
+        // 1. earlier tiles of this super tile
+        bool done = false;
+        for (;;)
+        {
+            const bool inq = lane < nq;
+            const uint64_t inv = __ballot(inq && !flag_valid(ft, c.epoch));
+            const uint64_t inc = __ballot(inq && flag_valid(ft, c.epoch)
+                                          && flag_inc(ft));
+            const int F = inc ? __builtin_ctzll(inc) : 64;
+            const uint64_t upto = F >= 63 ? ~0ull : ((2ull << F) - 1);
+            if ((inv & upto) == 0)
+            {
+                excl = wave_sum((inq && (int) lane <= F) ? (ft & kValMask)
+                                                         : 0ull);
+                done = inc != 0;
+                break;
+            }
+            if (!spin(c, &spins))
+            {
+                done = true;
+                break;
+            }
+            poll_tiles(c);
+        }
+        // 2. super tiles before this one, back to an inclusive one
+        for (uint32_t back = 0; !done;)
+        {
+            const uint64_t inv = __ballot(!flag_valid(fs, c.epoch));
+            const uint64_t inc = __ballot(flag_valid(fs, c.epoch) && flag_inc(fs));
+            const int G = inc ? __builtin_ctzll(inc) : 64;
+            const uint64_t upto = G >= 63 ? ~0ull : ((2ull << G) - 1);
+            if ((inv & upto) == 0)
+            {
+                excl += wave_sum((int) lane <= G ? (fs & kValMask) : 0ull);
+                if (inc)
+                    break;
+                fs = poll_supers(c, ++back);
+                continue;
+            }
+            if (!spin(c, &spins))
+                break;
+            fs = poll_supers(c, back);
+        }
+        if (lane == 0)
+            __hip_atomic_store(&c.flags[tile],
+                               kFlagInc | ep(c) | ((excl + total) & kValMask),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tile == f0 + in_super - 1)
+            publish_super(c, kFlagInc, excl + total);
+        return excl;
+    }
 };
 
-__device__ __forceinline__ Span
-unit_span(const uint8_t *in, const QH_LDS uint32_t *s_off, uint32_t lo,
-          uint32_t hi, uint32_t cap)
-{
-    Span sp;
-    const uintptr_t a = (uintptr_t) (in + s_off[lo]);
-    const uintptr_t b = (uintptr_t) (in + s_off[hi]);
-    sp.pa = a & ~(uintptr_t) 15;
-    const uintptr_t pb = (b + 15) & ~(uintptr_t) 15;
-    sp.n16 = (uint32_t) ((pb - sp.pa) >> 4);
-    sp.staged = pb - sp.pa <= (uintptr_t) cap;
-    return sp;
-}
+// ---- copy-out -------------------------------------------------------------
 
-// Units.  A tile's strings are coded in one or more consecutive units by the
-// workgroup that claimed it: a unit is the longest run of the tile's
-// remaining strings whose input fits the LDS stage (at least one string; a
-// single string longer than the stage is read from global memory).  With
-// header-sized strings a tile is one unit; the split keeps an oversized
-// tile from taking a slow path that would stall every look-back behind it.
-//
-// unit_vote: every thread votes for one candidate end (tid + 1); the unit
-// end is the largest candidate whose span fits.  *s_red must hold lo + 1
-// before the votes; read it after a barrier.
-__device__ __forceinline__ void
-unit_vote(const uint8_t *in, const QH_LDS uint32_t *s_off, uint32_t lo,
-          uint32_t cnt, uint32_t cap, QH_LDS uint32_t *s_red)
+// Copy of `total` bytes that sit at LDS byte offset 16 of a stage (16 bytes
+// of pad in front, 32 bytes of readable slack behind) to global `dst` (any
+// alignment), split so the stage can be refilled between reading it and
+// storing: gather() reads every chunk this lane stores into registers,
+// store() writes them (16-byte aligned stores; the partial first and last
+// chunks byte by byte).  NCH chunks per lane cover 64 * NCH * 16 bytes.
+template <int NCH>
+struct CopyOut
 {
-    const uint32_t j = threadIdx.x + 1;
-    bool fits = false;
-    if (j > lo + 1 && j <= cnt)
+    u32x4 o[NCH];
+    uint8_t *g0;
+    uint32_t r, nchunk, total;
+
+    __device__ __forceinline__ void gather(const QH_LDS uint32_t *s_stage,
+                                           uint8_t *dst, uint32_t tot)
     {
-        const uintptr_t pa = (uintptr_t) (in + s_off[lo]) & ~(uintptr_t) 15;
-        const uintptr_t pb = ((uintptr_t) (in + s_off[j]) + 15) & ~(uintptr_t) 15;
-        fits = pb - pa <= (uintptr_t) cap;
-    }
-    // fits is monotone in j: one LDS atomic per wave, for its last fit
-    const uint64_t m = __ballot(fits);
-    if (m && (threadIdx.x & 63) == 0)
-        __hip_atomic_fetch_max(s_red, (threadIdx.x & ~63u) + 64 - __builtin_clzll(m),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Residency census (diagnostic launch, kDbgCensus): every workgroup counts
-// itself in (arrivals, live), waits (bounded) until the whole grid has
-// arrived, then counts itself out.  The peak of `live` is the number of
-// workgroups that were on the device together.  Words: err[1] live,
-// err[2] peak, err[3] arrivals.
-__device__ __forceinline__ void
-census(const Coord &c)
-{
-    if (threadIdx.x != 0)
-        return;
-    const uint32_t live = __hip_atomic_fetch_add(&c.err[1], 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT) + 1;
-    __hip_atomic_fetch_max(&c.err[2], live, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t v = __hip_atomic_fetch_add(&c.err[3], 1u, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT) + 1;
-    for (uint32_t spins = 0; v < gridDim.x && spins < (1u << 14); ++spins)
-    {
-        __builtin_amdgcn_s_sleep(2);
-        v = __hip_atomic_load(&c.err[3], __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __hip_atomic_fetch_sub(&c.err[1], 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Dynamic tile order.  Workgroups form kGroups groups (blockIdx mod
-// kGroups); group g owns tiles g, g + NG, g + 2 NG, ... (NG = min(kGroups,
-// grid)) and its workgroups claim them in order from the group's counter.
-// A look-back then only waits on tiles that a running workgroup holds or
-// that its group will claim next, as long as every group has a running
-// workgroup -- not that the whole grid is resident.  Spreading the claims
-// over kGroups counters keeps same-address atomics from serialising.
-// Launch `epoch` uses counter set epoch & 1 and clears the other set for
-// the next launch on the stream (a context's launches are stream-ordered).
-constexpr uint32_t kGroups = 64;
-constexpr uint32_t kCtrStride = 64;        // u32 per counter: 256 B apart, so
-                                           // groups never share a cache line
-
-__device__ __forceinline__ uint32_t
-claim_tile(const Coord &c, uint32_t prev)
-{
-    if (c.dbg & kDbgStatic)
-    {
-        const uint64_t t = (uint64_t) prev + gridDim.x;
-        return t < c.n_tiles ? (uint32_t) t : c.n_tiles;
-    }
-    const uint32_t ng = gridDim.x < kGroups ? gridDim.x : kGroups;
-    const uint32_t g = blockIdx.x % ng;
-    const uint32_t k = __hip_atomic_fetch_add(
-        &c.ctr[((c.epoch & 1) * kGroups + g) * kCtrStride], 1u,
-        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t t = g + (uint64_t) k * ng;
-    return t < c.n_tiles ? (uint32_t) t : c.n_tiles;
-}
-
-// prologue: the first two tiles of this workgroup (every thread calls it)
-__device__ __forceinline__ void
-claim_first(const Coord &c, uint32_t *tile, uint32_t *next)
-{
-    __shared__ uint32_t s_pro[2];
-    if (blockIdx.x == 0 && threadIdx.x < kGroups)
-        __hip_atomic_store(
-            &c.ctr[(((c.epoch + 1) & 1) * kGroups + threadIdx.x) * kCtrStride],
-            0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0)
-    {
-        const uint32_t a = (c.dbg & kDbgStatic) ? blockIdx.x : claim_tile(c, 0);
-        const uint32_t b = claim_tile(c, a);
-        s_pro[0] = a < b ? a : b;
-        s_pro[1] = a < b ? b : a;
-    }
-    __syncthreads();
-    *tile = s_pro[0];
-    *next = s_pro[1];
-}
-
-// Each wave adds its strings' total output bytes to the tile accumulator
-// (wave count in [63:56], bytes below).  The wave that completes the count
-// of the tile's LAST unit publishes the tile aggregate and clears the
-// accumulator; after an earlier unit it only clears the count (bytes carry
-// over).  Read again only after barriers.  Once per wave, all lanes active.
-__device__ __forceinline__ void
-publish_wave_total(const Coord &c, uint32_t tile, uint32_t my_bytes,
-                   bool last_unit, QH_LDS unsigned long long *s_acc)
-{
-    uint64_t v = my_bytes;
+        total = tot;
+        r = (uint32_t) ((uintptr_t) dst & 15);
+        g0 = dst - r;                          // 16-byte aligned
+        nchunk = tot ? (r + tot + 15) >> 4 : 0;
+        // global chunk k holds stage bytes [16 + 16k - r, +16)
+        const uint32_t sh = (16 - r) & 15;     // byte shift inside the stage
+        const uint32_t c0 = (16 - r) >> 4;     // 1 when r == 0, else 0
+        const uint32_t q = sh >> 2, bs = sh & 3;
+        const QH_LDS uint32_t *s = s_stage + 4 * c0 + q;
+        const uint32_t lane = lane_id();
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1)
-        v += __shfl_xor(v, d, 64);
-    if ((threadIdx.x & 63) == 0)
-    {
-        const uint64_t inc = (1ull << 56) + v;
-        const uint64_t old = __hip_atomic_fetch_add(s_acc, inc, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-        if ((old >> 56) == (uint64_t) (kBlock / 64 - 1))
+        for (int j = 0; j < NCH; ++j)
         {
-            const uint64_t agg = (old + inc) & ((1ull << 56) - 1);
-            *s_acc = last_unit ? 0 : agg;
-            if (last_unit)
-                __hip_atomic_store(&c.flags[tile],
-                                   kFlagAgg | ((uint64_t) c.epoch << 40)
-                                            | (agg & kValMask),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// Copy `total` bytes that sit at LDS byte offset 16 (s_stage has 16 bytes of
-// pad in front) to global `dst` (any alignment) with 16-byte aligned stores;
-// the partial first/last 16-byte chunks are written byte by byte.  Called by
-// every thread of the block.
-__device__ __forceinline__ void
-copy_out(const QH_LDS uint32_t *s_stage, uint8_t *dst, uint32_t total)
-{
-    if (total == 0)
-        return;
-    const uint32_t r = (uint32_t) ((uintptr_t) dst & 15);
-    uint8_t *g0 = dst - r;                   // 16-byte aligned
-    const uint32_t nchunk = (r + total + 15) >> 4;
-    // global chunk k holds stage bytes [16 + 16k - r, +16)
-    const uint32_t sh = (16 - r) & 15;       // byte shift inside the stage
-    const uint32_t c0 = (16 - r) >> 4;       // 1 when r == 0, else 0
-    const QH_LDS u32x4 *s4 = (const QH_LDS u32x4 *) s_stage;
-    for (uint32_t k = threadIdx.x; k < nchunk; k += kBlock)
-    {
-        u32x4 a = s4[k + c0], b = s4[k + c0 + 1];
-        uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        uint32_t q = sh >> 2, bs = sh & 3;
-        u32x4 o;
-        // q is uniform across the workgroup
-        switch (q)
-        {
-        case 0: o = (u32x4){align_bytes(d[1], d[0], bs), align_bytes(d[2], d[1], bs),
-                            align_bytes(d[3], d[2], bs), align_bytes(d[4], d[3], bs)}; break;
-        case 1: o = (u32x4){align_bytes(d[2], d[1], bs), align_bytes(d[3], d[2], bs),
-                            align_bytes(d[4], d[3], bs), align_bytes(d[5], d[4], bs)}; break;
-        case 2: o = (u32x4){align_bytes(d[3], d[2], bs), align_bytes(d[4], d[3], bs),
-                            align_bytes(d[5], d[4], bs), align_bytes(d[6], d[5], bs)}; break;
-        default: o = (u32x4){align_bytes(d[4], d[3], bs), align_bytes(d[5], d[4], bs),
-                             align_bytes(d[6], d[5], bs), align_bytes(d[7], d[6], bs)}; break;
-        }
-        const uint32_t lo = k == 0 ? r : 0;
-        const uint32_t hi = (k == nchunk - 1) ? r + total - 16 * k : 16;
-        if (lo == 0 && hi == 16)
-            *(QH_GLB u32x4 *) (g0 + 16 * k) = o;
-        else
-        {
-            for (uint32_t b2 = lo; b2 < hi; ++b2)
+            const uint32_t k = lane + 64u * j;
+            if (k < nchunk)
             {
-                uint32_t q2 = b2 >> 2;
-                uint32_t wv = q2 == 0 ? o.x : q2 == 1 ? o.y : q2 == 2 ? o.z : o.w;
-                g0[16 * k + b2] = (uint8_t) (wv >> (8 * (b2 & 3)));
+                const QH_LDS uint32_t *p = s + 4 * k;
+                const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3],
+                               d4 = p[4];
+                o[j] = (u32x4){align_bytes(d1, d0, bs), align_bytes(d2, d1, bs),
+                               align_bytes(d3, d2, bs), align_bytes(d4, d3, bs)};
             }
         }
     }
-}
+    __device__ __forceinline__ void store() const
+    {
+        const uint32_t lane = lane_id();
+#pragma unroll
+        for (int j = 0; j < NCH; ++j)
+        {
+            const uint32_t k = lane + 64u * j;
+            if (k < nchunk)
+            {
+                const uint32_t lo = k == 0 ? r : 0;
+                const uint32_t hi = (k == nchunk - 1) ? r + total - 16 * k : 16;
+                if (lo == 0 && hi == 16)
+                    *(QH_GLB u32x4 *) (g0 + 16 * k) = o[j];
+                else
+                {
+                    const u32x4 v = o[j];
+                    for (uint32_t b = lo; b < hi; ++b)
+                    {
+                        const uint32_t qq = b >> 2;
+                        const uint32_t wv = qq == 0 ? v.x : qq == 1 ? v.y
+                                          : qq == 2 ? v.z : v.w;
+                        ((QH_GLB uint8_t *) g0)[16 * k + b] =
+                            (uint8_t) (wv >> (8 * (b & 3)));
+                    }
+                }
+            }
+        }
+    }
+};
 
 }  // namespace qhuff

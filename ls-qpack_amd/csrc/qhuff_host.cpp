@@ -29,19 +29,19 @@ struct qhuff_ctx
 {
     int device;
     int n_cu;
-    uint32_t enc_grid_max, dec_grid_max; // resident workgroups (persistent)
+    uint32_t enc_grid, dec_grid;         // workgroups per launch
     hipStream_t own_stream;
     DevTables *tab;                      // device
     LongParams lp;
-    unsigned long long *flags;           // device, cap_tiles entries
+    unsigned long long *flags;           // device look-back workspace:
+                                         // tile flags [cap_tiles], super
+                                         // flags [cap_super], super
+                                         // accumulators [2][cap_super]
     uint32_t *err;                       // device: [0] error word, [1..3]
                                          // census, then claim counters
-    uint64_t cap_tiles;
+    uint64_t cap_tiles, cap_super;
     uint32_t epoch;
     uint32_t dbg;                        // QHUFF_DEBUG ablation switches
-    const char *trace_path;              // QHUFF_TRACE phase-stamp dump
-    unsigned long long *trace;           // device, trace_cap stamps
-    uint64_t trace_cap;
     // host-path staging
     uint8_t *h_stage;                    // pinned
     size_t h_stage_cap;
@@ -50,22 +50,8 @@ struct qhuff_ctx
     char err_msg[256];
 };
 
-// device words: [0] error, [1..3] census, then the claim counters
+// device words: [0] error, then the claim counters
 constexpr size_t kErrWords = kCtrStride * (1 + 2 * kGroups);
-
-// blocks per CU that are certainly co-resident: the occupancy answer, no more
-// than the LDS allows at a 2 KiB allocation granule, and at least 1
-static int
-resident_blocks(int api, size_t lds_bytes, const hipDeviceProp_t &prop)
-{
-    const size_t gran = 2048;
-    size_t per_cu = prop.maxSharedMemoryPerMultiProcessor
-                  ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
-    size_t rounded = (lds_bytes + gran - 1) / gran * gran;
-    int by_lds = rounded ? (int) (per_cu / rounded) : api;
-    int b = api < by_lds ? api : by_lds;
-    return b < 1 ? 1 : b;
-}
 
 static int
 fail(qhuff_ctx *c, hipError_t e, const char *what)
@@ -123,21 +109,11 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         delete c;
         return rc ? rc : QHUFF_EDEVICE;
     }
-    // persistent grids: every workgroup must be resident (the look-back waits
-    // on lower tiles only, which are then always running or done).  The
-    // occupancy query is checked against LDS rounded up to a conservative
-    // allocation granule, and capped by the SGPR-admission rule of
-    // MI355X_MICROARCH.md (sec. Residency and cooperative launch).
-    occ_e = resident_blocks(occ_e, encode_lds_bytes(), prop);
-    occ_d = resident_blocks(occ_d, decode_lds_bytes(), prop);
-    c->enc_grid_max = (uint32_t) (occ_e * c->n_cu);
-    c->dec_grid_max = (uint32_t) (occ_d * c->n_cu);
-    // one look-back poll covers kLbWin predecessors; with grid <= kLbWin it
-    // always reaches the workgroup's own previous tile
-    if (c->enc_grid_max > (uint32_t) kLbWin)
-        c->enc_grid_max = (uint32_t) kLbWin;
-    if (c->dec_grid_max > (uint32_t) kLbWin)
-        c->dec_grid_max = (uint32_t) kLbWin;
+    // Every wave claims tiles until the batch is done (claims never wait on
+    // an unstarted wave, so the grid need not be co-resident): one full
+    // round of resident workgroups.
+    c->enc_grid = (uint32_t) (occ_e * c->n_cu);
+    c->dec_grid = (uint32_t) (occ_d * c->n_cu);
     e = hipMalloc((void **) &c->tab, sizeof(DevTables));
     if (e != hipSuccess)
     {
@@ -162,15 +138,15 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     {
         const char *d = getenv("QHUFF_DEBUG");
         c->dbg = d ? (uint32_t) strtoul(d, nullptr, 0) : 0;
-        c->trace_path = getenv("QHUFF_TRACE");
         const char *g = getenv("QHUFF_GRID_WG_PER_CU");  // tuning override
         if (g)
         {
             uint32_t k = (uint32_t) strtoul(g, nullptr, 0);
-            if (k >= 1 && k <= (uint32_t) occ_e)
-                c->enc_grid_max = k * c->n_cu;
-            if (k >= 1 && k <= (uint32_t) occ_d)
-                c->dec_grid_max = k * c->n_cu;
+            if (k >= 1)
+            {
+                c->enc_grid = k * c->n_cu;
+                c->dec_grid = k * c->n_cu;
+            }
         }
     }
     *ctx_out = c;
@@ -194,8 +170,6 @@ qhuff_close(qhuff_ctx *c)
         (void) hipFree(c->err);
     if (c->d_stage)
         (void) hipFree(c->d_stage);
-    if (c->trace)
-        (void) hipFree(c->trace);
     if (c->h_stage)
         (void) hipHostFree(c->h_stage);
     if (c->own_stream)
@@ -223,6 +197,18 @@ qhuff_device_error(qhuff_ctx *c)
     return (int) v;
 }
 
+extern "C" int
+qhuff_debug_clock(qhuff_ctx *c, uint64_t *out, uint32_t n)
+{
+    if (!c || !out || n > (uint32_t) kPhases)
+        return QHUFF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(out, c->err + 16, 8 * n, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemset(c->err + 16, 0, 8 * kPhases));
+    return QHUFF_OK;
+}
+
 extern "C" uint64_t
 qhuff_encode_bound(uint64_t in_bytes, uint32_t n, unsigned mode)
 {
@@ -241,7 +227,15 @@ qhuff_decode_bound(uint64_t in_bytes, uint32_t n)
     return in_bytes * 8 / 5 + 16;
 }
 
-// make room for the look-back flags of `tiles` tiles and advance the epoch
+static size_t
+lb_bytes(uint64_t cap_tiles, uint64_t cap_super)
+{
+    return 8 * (cap_tiles + 3 * cap_super);
+}
+
+// make room for the look-back workspace of `tiles` tiles and advance the
+// epoch (flags are epoch-tagged; the claim counters and super accumulators
+// of a launch are cleared by the launch before it)
 static int
 prepare_launch(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
 {
@@ -254,16 +248,19 @@ prepare_launch(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
             c->flags = nullptr;
         }
         uint64_t cap = tiles < 4096 ? 4096 : tiles;
-        HIPCHK(c, hipMalloc((void **) &c->flags, cap * 8));
-        HIPCHK(c, hipMemsetAsync(c->flags, 0, cap * 8, st));
+        uint64_t caps = (cap + kSuper - 1) / kSuper;
+        HIPCHK(c, hipMalloc((void **) &c->flags, lb_bytes(cap, caps)));
+        HIPCHK(c, hipMemsetAsync(c->flags, 0, lb_bytes(cap, caps), st));
         c->cap_tiles = cap;
+        c->cap_super = caps;
     }
     c->epoch = (c->epoch + 1) & kEpochMask;
     if (c->epoch == 0)
     {
-        // wrapped: stale flags could alias the new epoch, and the claim
-        // counter of epoch 1 was last used, not cleared
-        HIPCHK(c, hipMemsetAsync(c->flags, 0, c->cap_tiles * 8, st));
+        // wrapped: stale flags could alias the new epoch, and the counters
+        // of epoch 1 were last used, not cleared
+        HIPCHK(c, hipMemsetAsync(c->flags, 0, lb_bytes(c->cap_tiles, c->cap_super),
+                                 st));
         HIPCHK(c, hipMemsetAsync(c->err + kCtrStride, 0,
                                  2 * kGroups * kCtrStride * sizeof(uint32_t), st));
         c->epoch = 1;
@@ -272,92 +269,19 @@ prepare_launch(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
 }
 
 static Coord
-coord(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
+coord(qhuff_ctx *c, uint64_t tiles)
 {
     Coord k;
-    k.trace = nullptr;
-    if (c->trace_path)
-    {
-        if (c->trace_cap < kTraceSlots * tiles)
-        {
-            if (c->trace)
-                (void) hipFree(c->trace);
-            c->trace = nullptr;
-            c->trace_cap = 0;
-            if (hipMalloc((void **) &c->trace, 8 * kTraceSlots * tiles) == hipSuccess)
-                c->trace_cap = kTraceSlots * tiles;
-        }
-        if (c->trace)
-        {
-            (void) hipMemsetAsync(c->trace, 0, 8 * kTraceSlots * tiles, st);
-            k.trace = c->trace;
-        }
-    }
     k.flags = c->flags;
+    k.sflags = c->flags + c->cap_tiles;
+    k.sacc = k.sflags + c->cap_super;
+    k.cap_super = (uint32_t) c->cap_super;
     k.err = c->err;
     k.ctr = c->err + kCtrStride;
     k.epoch = c->epoch;
     k.n_tiles = (uint32_t) tiles;
     k.dbg = c->dbg;
     return k;
-}
-
-extern "C" int
-qhuff_residency(qhuff_ctx *c, int which, uint32_t grid, uint32_t *resident)
-{
-    if (!c || !resident || grid == 0 || (which != 0 && which != 1))
-        return QHUFF_EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
-    hipStream_t st = c->own_stream;
-    HIPCHK(c, hipMemsetAsync(c->err + 1, 0, 3 * sizeof(uint32_t), st));
-    Coord k = coord(c, grid, st);
-    k.dbg = kDbgCensus;
-    k.trace = nullptr;
-    if (which == 0)
-    {
-        EncArgs a = {};
-        a.c = k;
-        HIPCHK(c, launch_encode(a, grid, st));
-    }
-    else
-    {
-        DecArgs a = {};
-        a.c = k;
-        HIPCHK(c, launch_decode(a, grid, st));
-    }
-    HIPCHK(c, hipStreamSynchronize(st));
-    uint32_t v[2] = {0, 0};
-    HIPCHK(c, hipMemcpy(v, c->err + 1, sizeof(v), hipMemcpyDeviceToHost));
-    *resident = v[1];
-    return QHUFF_OK;
-}
-
-// diagnostic only (QHUFF_TRACE=path): synchronises, appends one record
-// {u32 'QTR2', kind, tiles, grid, slots, tiles * slots u64 stamps}
-static void
-dump_trace(qhuff_ctx *c, uint32_t kind, uint64_t tiles, uint32_t grid,
-           hipStream_t st)
-{
-    const size_t bytes = 8 * kTraceSlots * tiles;
-    if (!c->trace || c->trace_cap < kTraceSlots * tiles)
-        return;
-    unsigned long long *h = (unsigned long long *) malloc(bytes);
-    if (!h)
-        return;
-    if (hipMemcpyAsync(h, c->trace, bytes, hipMemcpyDeviceToHost, st) == hipSuccess
-            && hipStreamSynchronize(st) == hipSuccess)
-    {
-        FILE *f = fopen(c->trace_path, "ab");
-        if (f)
-        {
-            const uint32_t hdr[5] = {0x32525451u, kind, (uint32_t) tiles, grid,
-                                     (uint32_t) kTraceSlots};
-            (void) fwrite(hdr, sizeof(hdr), 1, f);
-            (void) fwrite(h, 8 * kTraceSlots, tiles, f);
-            fclose(f);
-        }
-    }
-    free(h);
 }
 
 extern "C" int
@@ -376,7 +300,7 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
         HIPCHK(c, hipMemsetAsync(out_off, 0, 4, st));
         return QHUFF_OK;
     }
-    uint64_t tiles = (n + kTile - 1) / kTile;
+    uint64_t tiles = (n + kWT - 1) / kWT;
     int rc = prepare_launch(c, tiles, st);
     if (rc)
         return rc;
@@ -388,10 +312,11 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.enc = c->tab->enc;
     a.n = n;
     a.mode = mode;
-    a.c = coord(c, tiles, st);
-    uint32_t grid = (uint32_t) (tiles < c->enc_grid_max ? tiles : c->enc_grid_max);
+    a.c = coord(c, tiles);
+    const uint64_t wpb = (uint64_t) encode_waves_per_block();
+    const uint64_t need = (tiles + wpb - 1) / wpb;
+    uint32_t grid = (uint32_t) (need < c->enc_grid ? need : c->enc_grid);
     HIPCHK(c, launch_encode(a, grid, st));
-    dump_trace(c, 0, tiles, grid, st);
     return QHUFF_OK;
 }
 
@@ -409,7 +334,7 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
         HIPCHK(c, hipMemsetAsync(out_off, 0, 4, st));
         return QHUFF_OK;
     }
-    uint64_t tiles = (n + kTile - 1) / kTile;
+    uint64_t tiles = (n + kWT - 1) / kWT;
     int rc = prepare_launch(c, tiles, st);
     if (rc)
         return rc;
@@ -422,11 +347,12 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.win = c->tab->win;
     a.sorted = c->tab->sorted;
     a.n = n;
-    a.c = coord(c, tiles, st);
+    a.c = coord(c, tiles);
     a.lp = c->lp;
-    uint32_t grid = (uint32_t) (tiles < c->dec_grid_max ? tiles : c->dec_grid_max);
+    const uint64_t wpb = (uint64_t) decode_waves_per_block();
+    const uint64_t need = (tiles + wpb - 1) / wpb;
+    uint32_t grid = (uint32_t) (need < c->dec_grid ? need : c->dec_grid);
     HIPCHK(c, launch_decode(a, grid, st));
-    dump_trace(c, 1, tiles, grid, st);
     return QHUFF_OK;
 }
 

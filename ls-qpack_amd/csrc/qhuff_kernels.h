@@ -63,5 +63,7 @@ hipError_t encode_occupancy(int *blocks_per_cu);
 hipError_t decode_occupancy(int *blocks_per_cu);
 size_t encode_lds_bytes();
 size_t decode_lds_bytes();
+int encode_waves_per_block();
+int decode_waves_per_block();
 
 }  // namespace qhuff

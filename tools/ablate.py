@@ -51,6 +51,24 @@ def main():
                 te.append(e0.elapsed_time(e1) * 1e3)
                 td.append(e1.elapsed_time(e2) * 1e3)
         err = c.device_error()
+        if v & 0x40:
+            c.debug_clock()
+            names = ["claim", "load", "codec", "scan+start", "compact/pack",
+                     "lookback", "copyout", "-"]
+            tiles = (n + 63) // 64
+            for which in ("enc", "dec"):
+                for it in range(10):
+                    if which == "enc":
+                        c.encode_into(d, o, n, 0, e_out, e_off, s)
+                    else:
+                        c.decode_into(h, ho, n, d_out, d_off, st, s)
+                torch.cuda.synchronize()
+                cl = c.debug_clock()
+                tot = sum(cl)
+                print("  %s cycles/tile by phase (wave-cycles): " % which
+                      + "  ".join("%s %.0f" % (nm, x / tiles / 10)
+                                  for nm, x in zip(names, cl) if x)
+                      + "   total %.0f" % (tot / tiles / 10), flush=True)
         c.close()
         res[v] = (float(np.median(te)), float(np.median(td)))
         print("dbg=%#5x  enc %8.1f us   dec %8.1f us  device_error %d"
