@@ -160,10 +160,10 @@ const char *qhuff_last_error(qhuff_ctx *ctx);
 #define QHUFF_DEVERR_SPIN 1
 int qhuff_device_error(qhuff_ctx *ctx);
 
-/* Diagnostic: synchronise and copy the context's kDbgClock per-phase cycle
- * sums (QHUFF_DEBUG=0x40 launches) into out[0..n) (n <= 8), then clear
- * them.  Returns QHUFF_OK or a negative QHUFF_E* code. */
-int qhuff_debug_clock(qhuff_ctx *ctx, uint64_t *out, uint32_t n);
+/* Diagnostic: in a QHUFF_PROFILE build (libqhuff_prof.so) copy up to
+ * max_words per-wave phase stamps of the last launch into dst and return
+ * the number available; 0 in normal builds.  Synchronous. */
+uint64_t qhuff_profile_read(qhuff_ctx *ctx, uint64_t *dst, uint64_t max_words);
 
 /* ---- multi-GPU sharding helpers (host arithmetic only) ----------------
  * Byte-balanced contiguous partition of a batch into g shards: writes

@@ -24,30 +24,28 @@
 // wave scan of the sizes they are compacted into the (now dead) input stage
 // and copied out with 16-byte stores once the look-back has resolved the
 // tile's output base.
-#include "qhuff_kernels.h"
+#include "qhuff_pipeline.h"
 
 namespace qhuff {
 
-constexpr int kDecWaves = 16;                          // waves per workgroup
-constexpr int kDecInCap = 3072;                        // staged input bytes
+constexpr int kDecInCap = kStageCap;                   // staged input bytes
 // byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
 // most 8/5 of its input, plus one byte written past the end by the
 // two-byte emitter
 constexpr int kArenaBytes = 2 * kWT + 8 * kDecInCap / 5 + 32;
-constexpr int kDecChunks = kDecInCap / 16 / 64;        // 16-B chunks per lane
-constexpr int kDecOutChunks = 3;                       // covers a stage of 3072 B
 
 struct DecWave                       // one wave's private LDS region
 {
     alignas(16) uint32_t in[kDecInCap / 4];   // BE input dwords; output stage
     alignas(16) uint8_t arena[kArenaBytes];
+    alignas(16) uint32_t hold[kStageCap / 4];  // the older pending tile's output
 };
 
 struct DecSmem
 {
     uint32_t win[kWinSize];
     uint16_t sorted[257];
-    DecWave w[kDecWaves];
+    DecWave w[kWaves];
 };
 
 struct DecLds                        // big-endian dwords staged in LDS
@@ -235,6 +233,110 @@ decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
     return bad ? -1 : (int) emit.n;
 }
 
+// Lean variant used by the staged (LDS) path.  The bit buffer is one 64-bit
+// register, MSB = next bit, holding >= 32 valid bits at every main step; the
+// dword that refills it is read one step ahead (`nx`), so only the window
+// lookup sits on the step's dependency chain.  Main steps run while a lane
+// has >= 32 real bits left (lanes past that are masked off); the EOS check
+// lives in the rare long-code branch.  The last < 32 bits take the padded
+// epilogue with the D3 tail rule, exactly as decode_string().
+template <class Emit>
+__device__ __forceinline__ int
+decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
+                  const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
+                  Emit &emit)
+{
+    uint32_t rem = bitend - bit0;            // real bits not yet consumed
+    uint64_t buf = 0;
+    uint32_t bits = 0, p = 0, nx = 0;
+    {
+        const uint32_t i0 = bit0 >> 5, sk = bit0 & 31;
+        const uint64_t ab = ((uint64_t) src[i0] << 32) | src[i0 + 1];
+        buf = ab << sk;
+        bits = 64 - sk;
+        p = i0 + 2;
+        nx = src[p];
+    }
+    uint32_t bad = 0;                        // (a u32: no lane-mask phis)
+    // one loop, no lane branches: a lane with < 32 real bits left steps with
+    // c = ns = 0 (its two arena byte writes land at its current end and are
+    // overwritten by the epilogue); the long-code fix is computed for the
+    // whole wave with selects, behind a wave-uniform branch
+    if (__builtin_amdgcn_ballot_w64(rem >= 32))
+    do
+    {
+        const bool act = rem >= 32;
+        const uint32_t hi = (uint32_t) (buf >> 32);
+        uint32_t e = s_win[hi >> (32 - kWinBits)];
+        uint32_t c = (e >> 16) & 15;          // bits of the entry's symbols
+        uint32_t ns = (e >> 24) & 3;          // symbols (0: longer code)
+        if (__builtin_amdgcn_ballot_w64(act & (e < (1u << 24))))
+        {
+            // a code of 13..30 bits (EOS rejects the string, D3 (a))
+            const bool lng = act & (e < (1u << 24));
+            uint32_t L;
+            const uint32_t sym = long_code(hi, s_sorted, &L);
+            const bool eos = lng & (sym == 256);
+            e = lng ? sym : e;
+            c = lng ? (eos ? 0u : L) : c;
+            ns = lng ? (eos ? 0u : 1u) : ns;
+            bad |= eos ? 1u : 0u;
+            rem = eos ? 0u : rem;
+        }
+        c = act ? c : 0u;
+        ns = act ? ns : 0u;
+        emit(e, ns);
+        buf <<= c;
+        bits -= c;
+        rem -= c;
+        const bool need = bits < 32;
+        const uint32_t dd = need ? nx : 0u;
+        buf |= (uint64_t) dd << ((32 - bits) & 31);
+        bits += need ? 32u : 0u;
+        p += need ? 1u : 0u;
+        nx = src[p];
+    } while (__builtin_amdgcn_ballot_w64(rem >= 32));
+
+    // epilogue: the last < 32 bits, padded with ones; D3 tail rule
+    bool fin = bad || rem == 0;
+    if (__builtin_amdgcn_ballot_w64(!fin))
+    do
+    {
+        const uint32_t hi = (uint32_t) (buf >> 32);
+        const uint32_t w = hi | (0xffffffffu >> (rem & 31));
+        const uint32_t e = s_win[w >> (32 - kWinBits)];
+        const uint32_t ns = (e >> 24) & 3, ct = (e >> 16) & 15,
+                       l0 = (e >> 20) & 15;
+        const bool two = (ns == 2) & (ct <= rem);
+        uint32_t c = two ? ct : (ns ? l0 : 31u);
+        uint32_t val = e;
+        bool eos = false;
+        if (__builtin_amdgcn_ballot_w64(!fin & (ns == 0) & (rem > kWinBits)))
+        {
+            uint32_t L;
+            const uint32_t sym = long_code(w, s_sorted, &L);
+            const bool lng = (ns == 0) & (rem > kWinBits);
+            c = lng ? L : c;
+            val = lng ? sym : val;
+            eos = lng & (sym == 256);
+        }
+        // c > rem: what is left is padding -- at most 7 bits of EOS prefix
+        const bool over = c > rem;
+        const uint32_t ones = 0xffffffffu >> ((32 - rem) & 31);
+        const bool tail_bad = rem >= 8 || (w >> ((32 - rem) & 31)) != ones;
+        const bool live = !fin;
+        bad |= (live & ((over & tail_bad) | (!over & eos))) ? 1u : 0u;
+        const bool step = live & !over & !eos;
+        const uint32_t nb = step ? (two ? 2u : 1u) : 0u;
+        c = step ? c : 0;
+        emit(val, nb);
+        buf <<= c;
+        rem -= c;
+        fin = fin | over | eos | (rem == 0);
+    } while (__builtin_amdgcn_ballot_w64(!fin));
+    return bad ? -1 : (int) emit.n;
+}
+
 // byte-granular arena sink: two unconditional byte stores per step (the
 // second is overwritten by the next step when only one symbol was emitted)
 struct ArenaEmit
@@ -272,27 +374,6 @@ struct GlobalEmit                            // slow path: byte stores
     }
 };
 
-// per-lane string bounds of a tile relative to its span
-struct LaneStr
-{
-    bool valid;
-    uint32_t rs, re;                 // byte positions relative to span.pa
-    uint32_t slot0;                  // arena slot
-};
-
-__device__ __forceinline__ LaneStr
-lane_str(const uint8_t *in, const TileOffs &to, uint32_t cnt, const Span &sp)
-{
-    LaneStr ls;
-    const uint32_t lane = lane_id();
-    ls.valid = lane < cnt;
-    const uint32_t A = to.first();
-    ls.rs = ls.valid ? (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa) : 0;
-    ls.re = ls.valid ? (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa) : 0;
-    ls.slot0 = 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
-    return ls;
-}
-
 // arena slot -> stage at byte D (wave-synchronous; other lanes write the
 // neighbouring bytes): bytes up to a dword boundary, whole dwords, tail
 __device__ __forceinline__ void
@@ -313,7 +394,124 @@ compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
         dstb[i] = src[i];
 }
 
-__global__ __launch_bounds__(64 * kDecWaves) void
+// A tile whose input or output does not fit the stage, coded eagerly:
+// input staged -> the arena already holds the bytes (sz / st given);
+// otherwise count from global memory, then decode again to global.  Out of
+// line (cold), state by value.
+__device__ __noinline__ void
+dec_slow_tile(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
+              uint32_t slot0, Coord c, uint32_t t, uint32_t cnt, TileOffs to,
+              Span sp, uint32_t sz, uint32_t st, uint8_t *out,
+              uint32_t *out_off, uint8_t *status, uint64_t n)
+{
+    const uint32_t lane = lane_id();
+    const bool valid = lane < cnt;
+    const uint32_t rs = valid ? (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa) : 0;
+    const uint32_t re = valid ? (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa) : 0;
+    const DecGlb src{(const QH_GLB uint32_t *) sp.pa};
+    if (!sp.staged)
+    {
+        int r = 0;
+        if (valid)
+        {
+            CountEmit em{0};
+            r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+        }
+        sz = r < 0 ? 0u : (uint32_t) r;
+        st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+    }
+    const uint32_t incl = wave_incl_scan(sz);
+    const uint32_t excl = incl - sz;
+    const uint32_t total = read_lane(incl, 63);
+    LookBack lb;
+    lb.start(c, t, total);
+    lb.super_agg(c);
+    lb.poll(c);
+    const uint64_t base = lb.finish(c);
+    uint8_t *dst = out + base + excl;
+    if (sp.staged)
+    {
+        const QH_LDS uint8_t *sa = wv->arena + slot0;
+        for (uint32_t i = 0; i < sz; ++i)
+            ((QH_GLB uint8_t *) dst)[i] = sa[i];
+    }
+    else if (valid && st == QHUFF_DEC_OK && sz)
+    {
+        GlobalEmit em{dst, 0};
+        decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+    }
+    const uint64_t s0 = (uint64_t) t * kWT;
+    if (valid)
+    {
+        ((QH_GLB uint32_t *) out_off)[s0 + lane] = (uint32_t) (base + excl);
+        ((QH_GLB uint8_t *) status)[s0 + lane] = (uint8_t) st;
+    }
+    if (t == c.n_tiles - 1 && lane == 0)
+        ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + total);
+}
+
+// the decode side of the wave pipeline (qhuff_pipeline.h)
+struct DecPolicy
+{
+    static constexpr bool kStatus = true;
+    const uint8_t *in;
+    QH_LDS DecSmem *sm;
+    QH_LDS DecWave *wv;
+    uint32_t slot0;                  // this lane's arena slot (current tile)
+
+    __device__ __forceinline__ void stage_in(const Chunks<kChunks> &ch,
+                                             const Span &sp)
+    {
+        ch.store<true>((QH_LDS u32x4 *) wv->in, sp.n16);
+    }
+    __device__ __forceinline__ const QH_LDS uint32_t *out_stage() const
+    {
+        return wv->in;
+    }
+    __device__ __forceinline__ QH_LDS uint32_t *hold() const
+    {
+        return wv->hold;
+    }
+    // staged tile: decode this lane's string into its arena slot
+    __device__ __forceinline__ void codec(const TileOffs &to, uint32_t cnt,
+                                          const Span &sp, uint32_t *sz,
+                                          uint32_t *st)
+    {
+        const uint32_t lane = lane_id();
+        const uint32_t A = to.first();
+        slot0 = 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
+        int r = 0;
+        if (lane < cnt)
+        {
+            const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
+            const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
+            ArenaEmit em{wv->arena + slot0, 0};
+            r = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted,
+                                  em);
+        }
+        *sz = r < 0 ? 0u : (uint32_t) r;
+        *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+    }
+    // arena -> the (dead) input stage, compacted
+    __device__ __forceinline__ void emit(uint32_t excl, uint32_t sz, uint32_t)
+    {
+        if (sz)
+            compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
+                           sz);
+    }
+
+    __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
+                                              TileOffs to, Span sp, uint32_t sz,
+                                              uint32_t st, uint8_t *out,
+                                              uint32_t *out_off, uint8_t *status,
+                                              uint64_t n)
+    {
+        dec_slow_tile(in, sm, wv, slot0, c, t, cnt, to, sp, sz, st, out,
+                      out_off, status, n);
+    }
+};
+
+__global__ __launch_bounds__(64 * kWaves) void
 qhuff_decode_kernel(DecArgs a)
 {
     __shared__ DecSmem smem;
@@ -322,7 +520,7 @@ qhuff_decode_kernel(DecArgs a)
     {
         const QH_GLB u32x4 *gw = (const QH_GLB u32x4 *) glb(a.win);
         QH_LDS u32x4 *sw = (QH_LDS u32x4 *) sm->win;
-        for (int i = tid; i < kWinSize / 4; i += 64 * kDecWaves)
+        for (int i = tid; i < kWinSize / 4; i += 64 * kWaves)
             sw[i] = gw[i];
         const QH_GLB uint16_t *gs = glb(a.sorted);
         if (tid < 257)
@@ -330,139 +528,14 @@ qhuff_decode_kernel(DecArgs a)
         clear_next_launch(a.c);
     }
     __syncthreads();                 // the only workgroup barrier
-
-    const uint32_t lane = lane_id();
-    QH_LDS DecWave *wv = &sm->w[tid >> 6];
-    QH_LDS uint32_t *stage = wv->in;
-    const QH_GLB uint32_t *gin_off = glb(a.in_off);
-    QH_GLB uint32_t *gout_off = glb(a.out_off);
-    QH_GLB uint8_t *gstat = glb(a.status);
-    const uint32_t n_waves = gridDim.x * kDecWaves;
-    const uint32_t gid = wave_gid(kDecWaves);
-    const uint32_t nt = a.c.n_tiles;
-    const uint32_t dbg = a.c.dbg;
-
-    auto tile_cnt = [&](uint32_t t) -> uint32_t {
-        return (uint32_t) min((uint64_t) kWT, a.n - (uint64_t) t * kWT);
-    };
-
-    // Tiles are claimed just in time: a wave claims its next tile only when
-    // it is about to code it, so claim order is processing order and a
-    // look-back only ever waits on tiles whose codec is already running.
-    // The claim -> offsets -> input latency of one wave hides under the
-    // codec work of the other waves on its SIMD.
-    PhaseClock clk;
-    clk.init(dbg);
-    for (;;)
-    {
-        const uint32_t t = claim_tile(a.c, gid, n_waves);
-        clk.lap(0);
-        if (t >= nt)
-            break;
-        const uint32_t cnt = tile_cnt(t);
-        TileOffs to;
-        to.load(gin_off, (uint64_t) t * kWT, cnt);
-        const Span sp = tile_span(a.in, to.first(), to.last(), kDecInCap);
-        if (sp.staged)
-        {
-            Chunks<kDecChunks> ch;
-            ch.load(sp);
-            ch.store<true>((QH_LDS u32x4 *) stage, sp.n16);
-        }
-        wave_sync();
-        clk.lap(1);
-
-        // 1. decode this tile (input staged in LDS, or read from global)
-        const LaneStr ls = lane_str(a.in, to, cnt, sp);
-        int r = 0;
-        if (ls.valid)
-        {
-            if (dbg & kDbgNoCodec)
-                r = (int) (ls.re - ls.rs);
-            else if (sp.staged)
-            {
-                ArenaEmit em{wv->arena + ls.slot0, 0};
-                r = decode_string(DecLds{stage}, 8 * ls.rs, 8 * ls.re, sm->win,
-                                  sm->sorted, em);
-            }
-            else
-            {
-                CountEmit em{0};
-                r = decode_string(DecGlb{(const QH_GLB uint32_t *) sp.pa},
-                                  8 * ls.rs, 8 * ls.re, sm->win, sm->sorted,
-                                  em);
-            }
-        }
-        const uint32_t sz = r < 0 ? 0u : (uint32_t) r;
-        const uint32_t incl = wave_incl_scan(sz);
-        const uint32_t excl = incl - sz;
-        clk.lap(2);
-        const uint32_t total = read_lane(incl, 63);
-
-        // 2. publish the aggregate, issue the first look-back poll
-        LookBack lb;
-        if (!(dbg & kDbgNoLookback))
-            lb.start(a.c, t, total);
-        clk.lap(3);
-
-        // 3. compaction: arena slots -> the (dead) input stage
-        const bool staged_out = sp.staged && total + 64 <= (uint32_t) kDecInCap;
-        wave_sync();
-        if (staged_out && sz && !(dbg & kDbgNoCodec))
-            compact_string(wv->arena + ls.slot0,
-                           (QH_LDS uint8_t *) stage + 16 + excl, sz);
-        wave_sync();
-
-        clk.lap(4);
-
-        // 4. output base
-        const uint64_t base = (dbg & kDbgNoLookback) ? (uint64_t) t << 13
-                            : lb.finish(a.c);
-        clk.lap(5);
-
-        // 5. copy-out (stage -> registers -> 16-byte stores)
-        CopyOut<kDecOutChunks> co;
-        if (staged_out)
-            co.gather(stage, a.out + base, total);
-        if (!(dbg & kDbgNoStore))
-        {
-            if (staged_out)
-                co.store();
-            else if (sz && sp.staged)
-            {
-                // output larger than the stage: arena -> global, bytes
-                const QH_LDS uint8_t *src = wv->arena + ls.slot0;
-                QH_GLB uint8_t *dst = (QH_GLB uint8_t *) (a.out + base + excl);
-                for (uint32_t i = 0; i < sz; ++i)
-                    dst[i] = src[i];
-            }
-            else if (sz && !(dbg & kDbgNoCodec))
-            {
-                // input larger than the stage: decode again, to global
-                GlobalEmit em{a.out + base + excl, 0};
-                decode_string(DecGlb{(const QH_GLB uint32_t *) sp.pa},
-                              8 * ls.rs, 8 * ls.re, sm->win, sm->sorted,
-                              em);
-            }
-            const uint64_t s0 = (uint64_t) t * kWT;
-            if (ls.valid)
-            {
-                gout_off[s0 + lane] = (uint32_t) (base + excl);
-                gstat[s0 + lane] = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
-            }
-            if (t == nt - 1 && lane == 0)
-                gout_off[a.n] = (uint32_t) (base + total);
-        }
-        wave_sync();
-        clk.lap(6);
-    }
-    clk.flush(a.c.err);
+    DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
+    tile_pipeline(pol, a.c, a.in, a.in_off, a.n, a.out, a.out_off, a.status);
 }
 
 hipError_t
 launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st)
 {
-    hipLaunchKernelGGL(qhuff_decode_kernel, dim3(grid), dim3(64 * kDecWaves),
+    hipLaunchKernelGGL(qhuff_decode_kernel, dim3(grid), dim3(64 * kWaves),
                        0, st, a);
     return hipGetLastError();
 }
@@ -472,13 +545,13 @@ decode_occupancy(int *blocks_per_cu)
 {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
         blocks_per_cu, reinterpret_cast<const void *>(qhuff_decode_kernel),
-        64 * kDecWaves, 0);
+        64 * kWaves, 0);
 }
 
 int
 decode_waves_per_block()
 {
-    return kDecWaves;
+    return kWaves;
 }
 
 size_t

@@ -3,20 +3,18 @@
 //
 // Execution model ("wave tiles"): a workgroup only exists to share one copy
 // of the static code tables in LDS.  After the single table-load barrier
-// every wave is an independent worker with a private LDS region; it claims
-// tiles of kWT = 64 strings (one string per lane), stages the tile's packed
-// input, runs the per-lane codec, scans the 64 output sizes with cross-lane
-// operations, resolves the tile's output base with a decoupled look-back
-// over per-tile flags, and copies the compacted output out with 16-byte
-// stores.  No workgroup barrier is ever taken inside the tile loop, so the
-// latency of one wave's loads / look-back polls hides under the codec work
-// of the other waves on its SIMD.
+// every wave is an independent worker with a private LDS region; it codes
+// tiles of kWT = 64 strings (one string per lane), scans the 64 output sizes
+// with cross-lane operations, resolves each tile's output base with a
+// two-level decoupled look-back and stores the compacted output with 16-byte
+// stores.  No workgroup barrier is taken inside the tile loop.
 //
-//   * explicit LDS / global address spaces (a generic pointer into LDS
-//     compiles to flat_load with global-memory latency)
-//   * wave scans, wave-level decoupled look-back with bounded spins
-//   * grouped dynamic tile claims (no residency assumption)
-//   * split copy-out: stage -> registers, then 16-byte aligned stores
+// Every global round trip is kept off a wave's critical path (see
+// qhuff_pipeline.h): tiles are assigned statically (tile k of wave g is
+// g + k * W), offsets are loaded two tiles ahead and input one tile ahead,
+// and a tile's look-back and stores are deferred until after the next
+// tile's codec -- its output waits in registers -- so polls find their
+// predecessors published and no wait drains freshly issued stores.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -30,6 +28,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWT = 64;                     // strings per wave tile
+constexpr int kWaves = 12;                  // waves per workgroup (both kernels)
 
 // Look-back flag word: [63:42] launch epoch, [41:40] state (1 aggregate,
 // 2 inclusive), [39:0] byte count.  Epoch on top: within a launch an
@@ -46,39 +45,19 @@ constexpr int kSuper = 64;                  // tiles per super tile
 constexpr uint64_t kAccOne = 1ull << 48;
 constexpr uint64_t kAccMask = kAccOne - 1;
 
-// ablation switches (timing experiments only; outputs are wrong when set)
-constexpr uint32_t kDbgNoLookback = 2;      // base = tile * 8 KiB
-constexpr uint32_t kDbgNoStore = 4;         // skip the global output stores
-constexpr uint32_t kDbgNoCodec = 8;         // skip the per-string codec loops
-
-constexpr uint32_t kDbgClock = 0x40;        // per-phase cycle sums (below)
-
 // error bits reported through Coord::err
 constexpr uint32_t kErrSpin = 1;            // look-back spin limit hit
 
-// Dynamic tile order.  Waves form kGroups groups (global wave id mod
-// kGroups); group g owns tiles g, g + NG, g + 2 NG, ... (NG = min(kGroups,
-// waves)) and its waves claim them in order from the group's counter.  A
-// tile is only ever claimed by a running wave, and every wave processes its
-// claimed tiles in increasing order, so the lowest unfinished tile always
-// makes progress: the look-back needs no residency guarantee.  Spreading the
-// claims over kGroups counters keeps same-address atomics from serialising.
-// Launch `epoch` uses counter set epoch & 1 and clears the other set for the
-// next launch on the stream (a context's launches are stream-ordered).
-constexpr uint32_t kGroups = 64;
-constexpr uint32_t kCtrStride = 64;         // u32 per counter: 256 B apart
-
 struct Coord
 {
+    unsigned long long *prof;               // QHUFF_PROFILE builds: stamps
     unsigned long long *flags;              // per-tile look-back flags
     unsigned long long *sflags;             // per-super-tile flags
     unsigned long long *sacc;               // super accumulators [2][cap_super]
     uint32_t *err;                          // sticky device error word
-    uint32_t *ctr;                          // claim counters [2][kGroups], strided
     uint32_t epoch;                         // launch tag carried in flags
     uint32_t n_tiles;
     uint32_t cap_super;                     // sacc entries per parity
-    uint32_t dbg;
 };
 
 __device__ __forceinline__ uint32_t
@@ -101,15 +80,16 @@ align_bytes(uint32_t hi, uint32_t lo, uint32_t sh)
 }
 
 __device__ __forceinline__ uint32_t
-uniform(uint32_t v)
-{
-    return __builtin_amdgcn_readfirstlane(v);
-}
-
-__device__ __forceinline__ uint32_t
 read_lane(uint32_t v, uint32_t lane)
 {
     return __builtin_amdgcn_readlane(v, lane);
+}
+
+__device__ __forceinline__ uint64_t
+read_lane64(uint64_t v, uint32_t lane)
+{
+    return ((uint64_t) read_lane((uint32_t) (v >> 32), lane) << 32)
+         | read_lane((uint32_t) v, lane);
 }
 
 // orders this wave's LDS accesses across lanes (LDS instructions of one
@@ -147,85 +127,58 @@ wave_sum(T v)
     return v;
 }
 
-// Per-phase cycle accounting (kDbgClock): each wave sums s_memtime deltas
-// per phase in registers and adds them once, at exit, to err[16 + 2 * ph]
-// (u64 pairs).  Phase list: see the kernels.
-constexpr int kPhases = 8;
-struct PhaseClock
-{
-    uint64_t t0;
-    uint64_t sum[kPhases];
-    bool on;
-
-    __device__ __forceinline__ void init(uint32_t dbg)
-    {
-        on = (dbg & kDbgClock) != 0;
-        for (int i = 0; i < kPhases; ++i)
-            sum[i] = 0;
-        t0 = on ? __builtin_amdgcn_s_memtime() : 0;
-    }
-    __device__ __forceinline__ void lap(int ph)
-    {
-        if (on)
-        {
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            sum[ph] += t - t0;
-            t0 = t;
-        }
-    }
-    __device__ __forceinline__ void flush(uint32_t *err) const
-    {
-        if (on && (threadIdx.x & 63) == 0)
-            for (int i = 0; i < kPhases; ++i)
-                atomicAdd((unsigned long long *) (err + 16 + 2 * i),
-                          (unsigned long long) sum[i]);
-    }
-};
-
-// ---- tile claims -------------------------------------------------------
-
-__device__ __forceinline__ uint32_t
-wave_gid(int waves_per_block)
-{
-    return blockIdx.x * (uint32_t) waves_per_block + (threadIdx.x >> 6);
-}
-
-// lane 0 claims; the returned tile id is wave-uniform (n_tiles = none)
-__device__ __forceinline__ uint32_t
-claim_tile(const Coord &c, uint32_t gid, uint32_t n_waves)
-{
-    const uint32_t ng = n_waves < kGroups ? n_waves : kGroups;
-    const uint32_t g = gid % ng;
-    uint32_t k = 0;
-    if (lane_id() == 0)
-        k = __hip_atomic_fetch_add(
-            &c.ctr[((c.epoch & 1) * kGroups + g) * kCtrStride], 1u,
-            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    k = uniform(k);
-    const uint64_t t = g + (uint64_t) k * ng;
-    return t < c.n_tiles ? (uint32_t) t : c.n_tiles;
-}
-
-// clears the claim counters and super accumulators of the next launch on
-// the stream (they use the other parity; every thread of the grid helps)
+// clears the super accumulators of the next launch on the stream (they use
+// the other parity; every thread of the grid helps; all of them, since the
+// next launch may hold more tiles than this one)
 __device__ __forceinline__ void
 clear_next_launch(const Coord &c)
 {
     const uint32_t par = (c.epoch + 1) & 1;
-    if (blockIdx.x == 0 && threadIdx.x < kGroups)
-        __hip_atomic_store(&c.ctr[(par * kGroups + threadIdx.x) * kCtrStride],
-                           0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // all of them: the next launch may hold more tiles than this one
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < c.cap_super;
          i += gridDim.x * blockDim.x)
         __hip_atomic_store(&c.sacc[(uint64_t) par * c.cap_super + i], 0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- profile stamps (QHUFF_PROFILE builds only) --------------------------
+// Stamp slot `ph` of iteration `it` of this wave: prof[(gid * kProfIters +
+// it) * kProfSlots + ph] = s_memtime.  Compiled out otherwise.
+constexpr int kProfIters = 16, kProfSlots = 10;
+__device__ __forceinline__ void
+prof_value(const Coord &c, uint32_t it, int ph, uint64_t v)
+{
+#ifdef QHUFF_PROFILE
+    if (c.prof && it < (uint32_t) kProfIters && (threadIdx.x & 63) == 0)
+    {
+        const uint64_t gid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        c.prof[(gid * kProfIters + it) * kProfSlots + ph] = v;
+    }
+#else
+    (void) c;
+    (void) it;
+    (void) ph;
+    (void) v;
+#endif
+}
+
+__device__ __forceinline__ void
+prof_stamp(const Coord &c, uint32_t it, int ph)
+{
+#ifdef QHUFF_PROFILE
+    prof_value(c, it, ph, __builtin_amdgcn_s_memtime());
+#else
+    (void) c;
+    (void) it;
+    (void) ph;
+#endif
+}
+
 // ---- tile offsets ------------------------------------------------------
 
 // Lane i holds the start offset of string i of the tile and of string i+1
-// (clamped to the tile end).  `cnt` strings, cnt in [1, 64].
+// (clamped to the tile end).  `cnt` strings, cnt in [1, 64].  Both loads are
+// issued by every lane (clamped index): a fixed instruction count keeps the
+// compiler's vmcnt waits exact.
 struct TileOffs
 {
     uint32_t o0, o1;
@@ -263,7 +216,8 @@ tile_span(const uint8_t *in, uint32_t A, uint32_t B, uint32_t cap)
 }
 
 // A tile's staged input held in registers between its load and its LDS
-// write: NCH 16-byte chunks per lane.
+// write: NCH 16-byte chunks per lane.  Every lane issues every load (index
+// clamped into the span), so the instruction count is fixed.
 template <int NCH>
 struct Chunks
 {
@@ -272,12 +226,12 @@ struct Chunks
     __device__ __forceinline__ void load(const Span &sp)
     {
         const uint32_t lane = lane_id();
+        const uint32_t last = sp.n16 ? sp.n16 - 1 : 0;
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
         {
             const uint32_t i = lane + 64u * k;
-            if (i < sp.n16)
-                ch[k] = ((const QH_GLB u32x4 *) sp.pa)[i];
+            ch[k] = ((const QH_GLB u32x4 *) sp.pa)[i < last ? i : last];
         }
     }
     template <bool SWAP>
@@ -307,14 +261,14 @@ struct Chunks
 // flag.  Tiles are therefore grouped into super tiles of kSuper consecutive
 // tiles.  After its codec a tile publishes its aggregate and adds it to its
 // super tile's accumulator; the tile whose add completes the count publishes
-// the super tile's aggregate.  A tile's exclusive prefix is then
+// the super tile's aggregate (at the top of its wave's next iteration, when
+// the add has long returned).  A tile's exclusive prefix is then
 //   (aggregates of the earlier tiles of its super tile, back to an
 //    inclusive one if there is one)
 // + (super aggregates back to an inclusive super flag),
 // one 64-wide window of each, polled together.  Only aggregates are waited
-// for, and those are published right after codecs that are already running
-// (tiles are claimed in order), so no wait chains through other look-backs.
-// The last tile of a super tile publishes the super tile's inclusive flag.
+// for, so no wait chains through other look-backs.  The last tile of a super
+// tile publishes the super tile's inclusive flag.
 
 __device__ __forceinline__ bool
 flag_valid(uint64_t f, uint32_t epoch)
@@ -331,36 +285,40 @@ flag_inc(uint64_t f)
 struct LookBack
 {
     uint32_t tile, s;
-    uint64_t total;
+    uint32_t total;
     uint64_t acc_old;            // returned by the super accumulator add (lane 0)
     uint64_t ft, fs;             // polled tile / super flags (one per lane)
+    uint32_t spins_seen;         // re-polls of the last finish() (profiling)
 
-    __device__ __forceinline__ uint64_t ep(const Coord &c) const
+    __device__ __forceinline__ static uint64_t ep(const Coord &c)
     {
         return (uint64_t) c.epoch << 42;
     }
-    __device__ __forceinline__ void poll_tiles(const Coord &c)
+    __device__ __forceinline__ uint64_t poll_tile(const Coord &c) const
     {
         const uint32_t lane = lane_id();
-        const uint32_t f0 = s * kSuper;
-        ft = (tile - f0 > lane) ? __hip_atomic_load(&c.flags[tile - 1 - lane],
-                                                    __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT)
-                                : 0ull;
+        const uint32_t nq = tile - s * kSuper;
+        // lanes past the super start re-read the nearest valid slot
+        const uint32_t q = lane < nq ? lane : (nq ? nq - 1 : 0);
+        const uint64_t f = __hip_atomic_load(&c.flags[nq ? tile - 1 - q : tile],
+                                             __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        return nq ? f : 0ull;
     }
     // super flags s-1-lane-64*back (before super 0: inclusive 0)
-    __device__ __forceinline__ uint64_t poll_supers(const Coord &c,
-                                                    uint32_t back) const
+    __device__ __forceinline__ uint64_t poll_super(const Coord &c,
+                                                   uint32_t back) const
     {
         const int64_t j = (int64_t) s - 1 - lane_id() - 64 * (int64_t) back;
-        return j < 0 ? (kFlagInc | ep(c))
-                     : __hip_atomic_load(&c.sflags[j], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t f = __hip_atomic_load(&c.sflags[j < 0 ? 0 : j],
+                                             __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        return j < 0 ? (kFlagInc | ep(c)) : f;
     }
 
-    // publish the aggregate, add to the super accumulator, issue the polls
+    // publish the aggregate, add to the super accumulator
     __device__ __forceinline__ void start(const Coord &c, uint32_t t,
-                                          uint64_t tot)
+                                          uint32_t tot)
     {
         tile = t;
         s = t / kSuper;
@@ -368,22 +326,34 @@ struct LookBack
         acc_old = 0;
         if (lane_id() == 0)
         {
-            __hip_atomic_store(&c.flags[t], kFlagAgg | ep(c) | (tot & kValMask),
+            __hip_atomic_store(&c.flags[t], kFlagAgg | ep(c) | tot,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             acc_old = __hip_atomic_fetch_add(
                 &c.sacc[(uint64_t) (c.epoch & 1) * c.cap_super + s],
                 kAccOne + tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        poll_tiles(c);
-        fs = poll_supers(c, 0);
     }
-
     __device__ __forceinline__ void publish_super(const Coord &c, uint64_t state,
                                                   uint64_t v) const
     {
         if (lane_id() == 0)
             __hip_atomic_fetch_max(&c.sflags[s], state | ep(c) | (v & kValMask),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the add that completed the super tile publishes its aggregate
+    __device__ __forceinline__ void super_agg(const Coord &c) const
+    {
+        const uint32_t f0 = s * kSuper;
+        const uint32_t in_super = c.n_tiles - f0 < (uint32_t) kSuper
+                                ? c.n_tiles - f0 : (uint32_t) kSuper;
+        const uint64_t old = read_lane64(acc_old, 0);
+        if ((old >> 48) == in_super - 1)
+            publish_super(c, kFlagAgg, (old + total) & kAccMask);
+    }
+    __device__ __forceinline__ void poll(const Coord &c)
+    {
+        ft = poll_tile(c);
+        fs = poll_super(c, 0);
     }
 
     __device__ __forceinline__ bool spin(const Coord &c, uint32_t *spins) const
@@ -394,34 +364,27 @@ struct LookBack
                 atomicOr(c.err, kErrSpin);
             return false;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(2);
         return true;
     }
 
-    // returns the exclusive prefix of the tile; publishes its inclusive one
+    // returns the exclusive prefix of the tile (polls issued by poll());
+    // publishes its inclusive one
     __device__ __forceinline__ uint64_t finish(const Coord &c)
     {
         const uint32_t lane = lane_id();
         const uint32_t f0 = s * kSuper;
-        const uint32_t in_super = c.n_tiles - f0 < (uint32_t) kSuper
-                                ? c.n_tiles - f0 : (uint32_t) kSuper;
-        // the add that completes the super tile publishes its aggregate
-        const uint64_t old = ((uint64_t) read_lane((uint32_t) (acc_old >> 32), 0) << 32)
-                           | read_lane((uint32_t) acc_old, 0);
-        if ((old >> 48) == in_super - 1)
-            publish_super(c, kFlagAgg, (old + total) & kAccMask);
-
+        const uint32_t nq = tile - f0;               // earlier tiles in super
         uint32_t spins = 0;
         uint64_t excl = 0;
-        const uint32_t nq = tile - f0;               // earlier tiles in super
         // 1. earlier tiles of this super tile
         bool done = false;
         for (;;)
         {
             const bool inq = lane < nq;
-            const uint64_t inv = __ballot(inq && !flag_valid(ft, c.epoch));
-            const uint64_t inc = __ballot(inq && flag_valid(ft, c.epoch)
-                                          && flag_inc(ft));
+            const bool v = flag_valid(ft, c.epoch);
+            const uint64_t inv = __ballot(inq && !v);
+            const uint64_t inc = __ballot(inq && v && flag_inc(ft));
             const int F = inc ? __builtin_ctzll(inc) : 64;
             const uint64_t upto = F >= 63 ? ~0ull : ((2ull << F) - 1);
             if ((inv & upto) == 0)
@@ -436,13 +399,14 @@ struct LookBack
                 done = true;
                 break;
             }
-            poll_tiles(c);
+            ft = poll_tile(c);
         }
         // 2. super tiles before this one, back to an inclusive one
         for (uint32_t back = 0; !done;)
         {
-            const uint64_t inv = __ballot(!flag_valid(fs, c.epoch));
-            const uint64_t inc = __ballot(flag_valid(fs, c.epoch) && flag_inc(fs));
+            const bool v = flag_valid(fs, c.epoch);
+            const uint64_t inv = __ballot(!v);
+            const uint64_t inc = __ballot(v && flag_inc(fs));
             const int G = inc ? __builtin_ctzll(inc) : 64;
             const uint64_t upto = G >= 63 ? ~0ull : ((2ull << G) - 1);
             if ((inv & upto) == 0)
@@ -450,92 +414,139 @@ struct LookBack
                 excl += wave_sum((int) lane <= G ? (fs & kValMask) : 0ull);
                 if (inc)
                     break;
-                fs = poll_supers(c, ++back);
+                fs = poll_super(c, ++back);
                 continue;
             }
             if (!spin(c, &spins))
                 break;
-            fs = poll_supers(c, back);
+            fs = poll_super(c, back);
         }
         if (lane == 0)
             __hip_atomic_store(&c.flags[tile],
                                kFlagInc | ep(c) | ((excl + total) & kValMask),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t in_super = c.n_tiles - f0 < (uint32_t) kSuper
+                                ? c.n_tiles - f0 : (uint32_t) kSuper;
         if (tile == f0 + in_super - 1)
             publish_super(c, kFlagInc, excl + total);
+        spins_seen = spins;
         return excl;
     }
 };
 
-// ---- copy-out -------------------------------------------------------------
+// ---- deferred output --------------------------------------------------------
 
-// Copy of `total` bytes that sit at LDS byte offset 16 of a stage (16 bytes
-// of pad in front, 32 bytes of readable slack behind) to global `dst` (any
-// alignment), split so the stage can be refilled between reading it and
-// storing: gather() reads every chunk this lane stores into registers,
-// store() writes them (16-byte aligned stores; the partial first and last
-// chunks byte by byte).  NCH chunks per lane cover 64 * NCH * 16 bytes.
+// A tile's compacted output (at most 64 * NCH * 16 bytes) held in registers
+// between its gather from the LDS stage and its store: lane l holds the
+// tile-local 16-byte chunks l, l + 64, ...  store() shifts them to the
+// alignment of the global destination with one cross-lane rotate per dword,
+// writes whole 16-byte chunks with dwordx4 stores and the partial first / last
+// chunk with one byte store (lanes 0-15 and 16-31), so a tile's stores are a
+// fixed number of instructions.
 template <int NCH>
-struct CopyOut
+struct TileOut
 {
     u32x4 o[NCH];
-    uint8_t *g0;
-    uint32_t r, nchunk, total;
 
-    __device__ __forceinline__ void gather(const QH_LDS uint32_t *s_stage,
-                                           uint8_t *dst, uint32_t tot)
+    __device__ __forceinline__ void gather(const QH_LDS uint32_t *stage)
     {
-        total = tot;
-        r = (uint32_t) ((uintptr_t) dst & 15);
-        g0 = dst - r;                          // 16-byte aligned
-        nchunk = tot ? (r + tot + 15) >> 4 : 0;
-        // global chunk k holds stage bytes [16 + 16k - r, +16)
-        const uint32_t sh = (16 - r) & 15;     // byte shift inside the stage
-        const uint32_t c0 = (16 - r) >> 4;     // 1 when r == 0, else 0
-        const uint32_t q = sh >> 2, bs = sh & 3;
-        const QH_LDS uint32_t *s = s_stage + 4 * c0 + q;
         const uint32_t lane = lane_id();
 #pragma unroll
         for (int j = 0; j < NCH; ++j)
-        {
-            const uint32_t k = lane + 64u * j;
-            if (k < nchunk)
-            {
-                const QH_LDS uint32_t *p = s + 4 * k;
-                const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3],
-                               d4 = p[4];
-                o[j] = (u32x4){align_bytes(d1, d0, bs), align_bytes(d2, d1, bs),
-                               align_bytes(d3, d2, bs), align_bytes(d4, d3, bs)};
-            }
-        }
+            o[j] = ((const QH_LDS u32x4 *) stage)[lane + 64 * j];
     }
-    __device__ __forceinline__ void store() const
+    __device__ __forceinline__ void park(QH_LDS uint32_t *hold) const
     {
         const uint32_t lane = lane_id();
 #pragma unroll
         for (int j = 0; j < NCH; ++j)
+            ((QH_LDS u32x4 *) hold)[lane + 64 * j] = o[j];
+    }
+
+    __device__ __forceinline__ void store(uint8_t *dst, uint32_t total) const
+    {
+        const uint32_t lane = lane_id();
+        const uint32_t r = (uint32_t) ((uintptr_t) dst & 15);
+        // wave-uniform 16-byte aligned base, 32-bit lane offsets
+        QH_GLB u32x4 *g4 = (QH_GLB u32x4 *) (dst - r);
+        QH_GLB uint8_t *g1 = (QH_GLB uint8_t *) (dst - r);
+        const uint32_t nch = total ? (r + total + 15) >> 4 : 0;  // global chunks
+        // global chunk j = tile bytes [16 j - r, 16 j - r + 16): the last r
+        // bytes of tile chunk j - 1 and the first 16 - r of tile chunk j
+        const uint32_t sh = (16 - r) & 15, q = sh >> 2, b = sh & 3;
+        u32x4 g[NCH];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j)
         {
-            const uint32_t k = lane + 64u * j;
-            if (k < nchunk)
+            u32x4 prev;
+            prev.x = __shfl_up(o[j].x, 1, 64);
+            prev.y = __shfl_up(o[j].y, 1, 64);
+            prev.z = __shfl_up(o[j].z, 1, 64);
+            prev.w = __shfl_up(o[j].w, 1, 64);
+            if (j == 0)
             {
-                const uint32_t lo = k == 0 ? r : 0;
-                const uint32_t hi = (k == nchunk - 1) ? r + total - 16 * k : 16;
-                if (lo == 0 && hi == 16)
-                    *(QH_GLB u32x4 *) (g0 + 16 * k) = o[j];
-                else
-                {
-                    const u32x4 v = o[j];
-                    for (uint32_t b = lo; b < hi; ++b)
-                    {
-                        const uint32_t qq = b >> 2;
-                        const uint32_t wv = qq == 0 ? v.x : qq == 1 ? v.y
-                                          : qq == 2 ? v.z : v.w;
-                        ((QH_GLB uint8_t *) g0)[16 * k + b] =
-                            (uint8_t) (wv >> (8 * (b & 3)));
-                    }
-                }
+                if (lane == 0)
+                    prev = (u32x4){0, 0, 0, 0};
+            }
+            else
+            {
+                const u32x4 p63 = (u32x4){read_lane(o[j - 1].x, 63),
+                                          read_lane(o[j - 1].y, 63),
+                                          read_lane(o[j - 1].z, 63),
+                                          read_lane(o[j - 1].w, 63)};
+                if (lane == 0)
+                    prev = p63;
+            }
+            const uint32_t d[8] = {prev.x, prev.y, prev.z, prev.w,
+                                   o[j].x, o[j].y, o[j].z, o[j].w};
+            // q is wave-uniform
+            switch (r == 0 ? 4 : q)
+            {
+            case 0: g[j] = (u32x4){align_bytes(d[1], d[0], b), align_bytes(d[2], d[1], b),
+                                   align_bytes(d[3], d[2], b), align_bytes(d[4], d[3], b)}; break;
+            case 1: g[j] = (u32x4){align_bytes(d[2], d[1], b), align_bytes(d[3], d[2], b),
+                                   align_bytes(d[4], d[3], b), align_bytes(d[5], d[4], b)}; break;
+            case 2: g[j] = (u32x4){align_bytes(d[3], d[2], b), align_bytes(d[4], d[3], b),
+                                   align_bytes(d[5], d[4], b), align_bytes(d[6], d[5], b)}; break;
+            case 3: g[j] = (u32x4){align_bytes(d[4], d[3], b), align_bytes(d[5], d[4], b),
+                                   align_bytes(d[6], d[5], b), align_bytes(d[7], d[6], b)}; break;
+            default: g[j] = o[j]; break;
             }
         }
+        const bool last_part = ((r + total) & 15) != 0;
+        const bool first_part = r != 0 || (nch == 1 && last_part);
+#pragma unroll
+        for (int j = 0; j < NCH; ++j)
+        {
+            const uint32_t k = lane + 64u * j;
+            const bool part = (k == 0 && first_part) || (k == nch - 1 && last_part);
+            if (k < nch && !part)
+                g4[k] = g[j];
+        }
+        // partial chunks: lanes 0-15 write bytes of chunk 0, lanes 16-31 bytes
+        // of chunk nch - 1 (when it is another partial chunk)
+        const uint32_t kl = nch ? nch - 1 : 0, jl = kl >> 6, ll = kl & 63;
+        u32x4 cl = g[0];
+#pragma unroll
+        for (int j = 1; j < NCH; ++j)
+            cl = jl == (uint32_t) j ? g[j] : cl;
+        const u32x4 c0 = (u32x4){read_lane(g[0].x, 0), read_lane(g[0].y, 0),
+                                 read_lane(g[0].z, 0), read_lane(g[0].w, 0)};
+        const u32x4 cz = (u32x4){read_lane(cl.x, ll), read_lane(cl.y, ll),
+                                 read_lane(cl.z, ll), read_lane(cl.w, ll)};
+        const bool lo_half = lane < 16;
+        const uint32_t bi = lane & 15;
+        const uint32_t kk = lo_half ? 0 : kl;
+        const u32x4 src = lo_half ? c0 : cz;
+        const uint32_t wsel = bi >> 2;
+        const uint32_t wv = wsel == 0 ? src.x : wsel == 1 ? src.y
+                          : wsel == 2 ? src.z : src.w;
+        const uint32_t gb = 16 * kk + bi;            // byte offset from g0
+        const bool in_range = gb >= r && gb < r + total;
+        const bool want = lane < 32 && in_range
+                       && (lo_half ? first_part : (last_part && kl != 0));
+        if (want)
+            g1[gb] = (uint8_t) (wv >> (8 * (bi & 3)));
     }
 };
 

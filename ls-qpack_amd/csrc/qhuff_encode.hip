@@ -20,27 +20,25 @@
 //      16-byte aligned global stores; out_off stores.
 // Tiles whose input or output does not fit the LDS stages take the same
 // steps with global reads / per-lane global writes (correct, slower).
-#include "qhuff_kernels.h"
+#include "qhuff_pipeline.h"
 
 namespace qhuff {
 
-constexpr int kEncWaves = 16;                 // waves per workgroup
-constexpr int kEncInCap = 3072;               // staged input bytes per tile
-constexpr int kEncOutCap = 3072;              // output stage bytes per tile
-constexpr int kEncChunks = kEncInCap / 16 / 64;
-constexpr int kEncOutChunks = 3;                 // covers a stage of 3072 B
+constexpr int kEncInCap = kStageCap;          // staged input bytes per tile
+constexpr int kEncOutCap = kStageCap;         // output stage bytes per tile
 
 struct EncWave                                // one wave's private LDS region
 {
     alignas(16) uint32_t in[kEncInCap / 4 + 4];
-    alignas(16) uint32_t out[kEncOutCap / 4];     // 16 B pad in front
+    alignas(16) uint32_t out[kEncOutCap / 4];
+    alignas(16) uint32_t hold[kStageCap / 4];  // the older pending tile's output
 };
 
 struct EncSmem
 {
     u32x2 enc[257];
     uint8_t len[256];
-    EncWave w[kEncWaves];
+    EncWave w[kWaves];
 };
 
 // source of aligned input dwords: LDS stage or global
@@ -164,8 +162,24 @@ byte_mask(uint32_t d, uint32_t d0, uint32_t dl, uint32_t rs, uint32_t re)
     return m;
 }
 
+// 4-bit valid-byte mask -> byte mask (0xff per set bit)
+__device__ __forceinline__ uint32_t
+mask_bytes(uint32_t m)
+{
+    return (m & 1 ? 0xffu : 0u) | (m & 2 ? 0xff00u : 0u)
+         | (m & 4 ? 0xff0000u : 0u) | (m & 8 ? 0xff000000u : 0u);
+}
+
+__device__ __forceinline__ uint32_t
+len4(uint32_t w, const QH_LDS uint8_t *s_len)
+{
+    return s_len[w & 0xff] | (s_len[(w >> 8) & 0xff] << 8)
+         | (s_len[(w >> 16) & 0xff] << 16) | (s_len[w >> 24] << 24);
+}
+
 // sum of code lengths over bytes [rs, re) (positions relative to the source):
-// four independent LDS lookups per dword, masked and summed with v_sad_u8
+// two dwords per iteration (independent LDS lookups in flight together),
+// four lengths packed per dword, masked and summed with v_sad_u8
 template <class Src>
 __device__ __forceinline__ uint32_t
 code_bits(const Src &src, uint32_t rs, uint32_t re, const QH_LDS uint8_t *s_len)
@@ -174,19 +188,16 @@ code_bits(const Src &src, uint32_t rs, uint32_t re, const QH_LDS uint8_t *s_len)
     if (re == rs)
         return 0;
     const uint32_t d0 = rs >> 2, dl = (re - 1) >> 2;
-    for (uint32_t d = d0; d <= dl; ++d)
+    for (uint32_t d = d0; d <= dl; d += 2)
     {
-        const uint32_t w = src.dw(d);
-        const uint32_t l0 = s_len[w & 0xff];
-        const uint32_t l1 = s_len[(w >> 8) & 0xff];
-        const uint32_t l2 = s_len[(w >> 16) & 0xff];
-        const uint32_t l3 = s_len[w >> 24];
-        const uint32_t m = byte_mask(d, d0, dl, rs, re);
-        // expand the 4-bit mask to bytes: 0x000000ff per set bit
-        const uint32_t bm = (m & 1 ? 0xffu : 0u) | (m & 2 ? 0xff00u : 0u)
-                          | (m & 4 ? 0xff0000u : 0u) | (m & 8 ? 0xff000000u : 0u);
-        const uint32_t packed = l0 | (l1 << 8) | (l2 << 16) | (l3 << 24);
-        bits = __builtin_amdgcn_sad_u8(packed & bm, 0u, bits);
+        const bool two = d + 1 <= dl;
+        const uint32_t w0 = src.dw(d);
+        const uint32_t w1 = two ? src.dw(d + 1) : 0u;
+        const uint32_t p0 = len4(w0, s_len), p1 = len4(w1, s_len);
+        const uint32_t m0 = mask_bytes(byte_mask(d, d0, dl, rs, re));
+        const uint32_t m1 = two ? mask_bytes(byte_mask(d + 1, d0, dl, rs, re)) : 0u;
+        bits = __builtin_amdgcn_sad_u8(p0 & m0, 0u, bits);
+        bits = __builtin_amdgcn_sad_u8(p1 & m1, 0u, bits);
     }
     return bits;
 }
@@ -217,6 +228,140 @@ pack_string(const Src &src, uint32_t rs, uint32_t re, bool raw,
         for (int b = 0; b < 4; ++b)
             pk.put(e[b].x, (m >> b) & 1 ? e[b].y : 0u);
     }
+}
+
+// ---- branch-free packing into the LDS stage ------------------------------
+//
+// The stage holds the tile's output as a big-endian bit stream in dwords
+// (byte-swapped words), zeroed before packing.  Every code is OR-ed in at its
+// bit position: the only loop-carried state is the position, there is no
+// data-dependent flush, and neighbouring strings (which share boundary
+// dwords) need no coordination.
+
+// OR the `len` (<= 32) low bits of v into the stream at bit `pos`
+__device__ __forceinline__ void
+or_bits(QH_LDS uint32_t *st, uint32_t pos, uint32_t v, uint32_t len)
+{
+    const uint32_t w = pos >> 5, o = pos & 31;
+    uint64_t x = len ? ((uint64_t) v << (64 - len)) : 0ull;   // left-aligned
+    x >>= o;
+    __hip_atomic_fetch_or(&st[w], bswap32((uint32_t) (x >> 32)),
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(&st[w + 1], bswap32((uint32_t) x),
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// E2 / E3 payload of bytes [rs, re) of the LDS input, from bit `pos`; four
+// input bytes per step: their codes are concatenated (at most 32 bits in the
+// common case -- every code of <= 8 bits, and raw bytes) and OR-ed in with
+// one two-dword OR; a wave-uniform branch takes any step with a longer
+// concatenation code by code.  Returns the end position.
+// codes of the (masked) bytes of one input dword
+__device__ __forceinline__ void
+codes4(uint32_t w, uint32_t m, bool raw, const QH_LDS u32x2 *s_enc,
+       uint32_t (&c)[4], uint32_t (&l)[4])
+{
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+    {
+        const uint32_t ch = (w >> (8 * b)) & 0xff;
+        const u32x2 t = s_enc[ch];
+        const bool on = (m >> b) & 1;
+        c[b] = on ? (raw ? ch : t.x) : 0u;
+        l[b] = on ? (raw ? 8u : t.y) : 0u;
+    }
+}
+
+// concatenation of four codes of at most 32 bits in total
+__device__ __forceinline__ uint32_t
+cat4(const uint32_t (&c)[4], const uint32_t (&l)[4])
+{
+    uint32_t v = c[0];
+    v = (l[1] ? v << l[1] : v) | c[1];
+    v = (l[2] ? v << l[2] : v) | c[2];
+    v = (l[3] ? v << l[3] : v) | c[3];
+    return v;
+}
+
+__device__ __forceinline__ uint32_t
+pack_bits(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, bool raw,
+          const QH_LDS u32x2 *s_enc, QH_LDS uint32_t *st, uint32_t pos)
+{
+    if (re == rs)
+        return pos;
+    const uint32_t d0 = rs >> 2, dl = (re - 1) >> 2;
+    for (uint32_t d = d0; d <= dl; d += 2)
+    {
+        const bool two = d + 1 <= dl;
+        const uint32_t w0 = in[d];
+        const uint32_t w1 = two ? in[d + 1] : 0u;
+        uint32_t c0[4], l0[4], c1[4], l1[4];
+        codes4(w0, byte_mask(d, d0, dl, rs, re), raw, s_enc, c0, l0);
+        codes4(w1, two ? byte_mask(d + 1, d0, dl, rs, re) : 0u, raw, s_enc,
+               c1, l1);
+        const uint32_t L0 = l0[0] + l0[1] + l0[2] + l0[3];
+        const uint32_t L1 = l1[0] + l1[1] + l1[2] + l1[3];
+        if (__builtin_amdgcn_ballot_w64(L0 > 32 || L1 > 32))
+        {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+            {
+                or_bits(st, pos, c0[b], l0[b]);
+                pos += l0[b];
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+            {
+                or_bits(st, pos, c1[b], l1[b]);
+                pos += l1[b];
+            }
+        }
+        else
+        {
+            or_bits(st, pos, cat4(c0, l0), L0);
+            pos += L0;
+            or_bits(st, pos, cat4(c1, l1), L1);
+            pos += L1;
+        }
+    }
+    return pos;
+}
+
+// literal framing + payload + EOS-prefix padding into the LDS stage, from
+// byte `start` (lsqpack.c:839-876, 5171-5189)
+__device__ __forceinline__ void
+emit_bits(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
+          bool huff, uint32_t plen, const QH_LDS u32x2 *s_enc,
+          QH_LDS uint32_t *st, uint32_t start)
+{
+    uint32_t pos = 8 * start;
+    if (mode)
+    {
+        const uint32_t mask = (1u << mode) - 1, first = huff ? (1u << mode) : 0;
+        if (plen < mask)
+        {
+            or_bits(st, pos, first | plen, 8);
+            pos += 8;
+        }
+        else
+        {
+            or_bits(st, pos, first | mask, 8);
+            pos += 8;
+            uint32_t v = plen - mask;
+            while (v >= 128)
+            {
+                or_bits(st, pos, 0x80 | (v & 0x7f), 8);
+                pos += 8;
+                v >>= 7;
+            }
+            or_bits(st, pos, v, 8);
+            pos += 8;
+        }
+    }
+    pos = pack_bits(in, rs, re, !huff, s_enc, st, pos);
+    const uint32_t pad = (8 - (pos & 7)) & 7;
+    if (pad)
+        or_bits(st, pos, (1u << pad) - 1, pad);
 }
 
 // literal framing (lsqpack.c:852-854, 862-864, 819-836): H bit + prefixed
@@ -257,28 +402,139 @@ struct EncSize
 
 template <class Src>
 __device__ __forceinline__ EncSize
-size_string(const EncArgs &a, const Src &src, uint32_t rs, uint32_t re,
+size_string(uint32_t mode, const Src &src, uint32_t rs, uint32_t re,
             const QH_LDS uint8_t *s_len)
 {
     EncSize z;
     const uint32_t len = re - rs;
-    const uint32_t hb = (a.c.dbg & kDbgNoCodec) ? len
-                      : (code_bits(src, rs, re, s_len) + 7) >> 3;
+    const uint32_t hb = (code_bits(src, rs, re, s_len) + 7) >> 3;
     z.huff = true;
     z.plen = 0;
-    if (a.mode == 0)
+    if (mode == 0)
         z.size = hb;
     else
     {
         z.huff = hb < len;                       // strict <, lsqpack.c:848
         z.plen = z.huff ? hb : len;
-        z.size = int_len(z.plen, a.mode) + z.plen;
+        z.size = int_len(z.plen, mode) + z.plen;
     }
     return z;
 }
 
 
-__global__ __launch_bounds__(64 * kEncWaves) void
+// A tile whose input or output does not fit the stages, coded eagerly:
+// sizes from the stage (given) or from global memory, then packed straight
+// to global memory.  Out of line (cold), state by value.
+__device__ __noinline__ void
+enc_slow_tile(const uint8_t *in, uint32_t mode, QH_LDS EncSmem *sm,
+              QH_LDS EncWave *wv, uint32_t rs, uint32_t re, EncSize z, Coord c,
+              uint32_t t, uint32_t cnt, TileOffs to, Span sp, uint32_t sz,
+              uint8_t *out, uint32_t *out_off, uint64_t n)
+{
+    const uint32_t lane = lane_id();
+    const bool valid = lane < cnt;
+    const EncGlb gsrc{(const QH_GLB uint32_t *) sp.pa};
+    if (!sp.staged)
+    {
+        rs = valid ? (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa) : 0;
+        re = valid ? (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa) : 0;
+        z = (EncSize){0, 0, true};
+        if (valid)
+            z = size_string(mode, gsrc, rs, re, sm->len);
+        sz = z.size;
+    }
+    const uint32_t incl = wave_incl_scan(sz);
+    const uint32_t excl = incl - sz;
+    const uint32_t total = read_lane(incl, 63);
+    LookBack lb;
+    lb.start(c, t, total);
+    lb.super_agg(c);
+    lb.poll(c);
+    const uint64_t base = lb.finish(c);
+    if (valid && sz)
+    {
+        const uint32_t adj = (uint32_t) ((uintptr_t) out & 3);
+        Packer<PackGlb> pk;
+        pk.sink.out = out - adj;
+        const uint32_t p0 = adj + (uint32_t) base + excl;
+        pk.init(p0, p0 + sz);
+        if (sp.staged)
+            emit_string(EncLds{wv->in}, rs, re, mode, z.huff, z.plen, sm->enc,
+                        pk);
+        else
+            emit_string(gsrc, rs, re, mode, z.huff, z.plen, sm->enc, pk);
+    }
+    const uint64_t s0 = (uint64_t) t * kWT;
+    if (valid)
+        ((QH_GLB uint32_t *) out_off)[s0 + lane] = (uint32_t) (base + excl);
+    if (t == c.n_tiles - 1 && lane == 0)
+        ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + total);
+}
+
+// the encode side of the wave pipeline (qhuff_pipeline.h)
+struct EncPolicy
+{
+    static constexpr bool kStatus = false;
+    const uint8_t *in;
+    uint32_t mode;                   // 0 payload, 3/5/7 literal prefix bits
+    QH_LDS EncSmem *sm;
+    QH_LDS EncWave *wv;
+    uint32_t rs, re;                 // this lane's string in the stage
+    EncSize z;
+
+    __device__ __forceinline__ void stage_in(const Chunks<kChunks> &ch,
+                                             const Span &sp)
+    {
+        ch.store<false>((QH_LDS u32x4 *) wv->in, sp.n16);
+    }
+    __device__ __forceinline__ const QH_LDS uint32_t *out_stage() const
+    {
+        return wv->out;
+    }
+    __device__ __forceinline__ QH_LDS uint32_t *hold() const
+    {
+        return wv->hold;
+    }
+    // staged tile: size this lane's string (E1, and the E3 choice)
+    __device__ __forceinline__ void codec(const TileOffs &to, uint32_t cnt,
+                                          const Span &sp, uint32_t *sz,
+                                          uint32_t *st)
+    {
+        const bool valid = lane_id() < cnt;
+        rs = valid ? (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa) : 0;
+        re = valid ? (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa) : 0;
+        z = (EncSize){0, 0, true};
+        if (valid)
+            z = size_string(mode, EncLds{wv->in}, rs, re, sm->len);
+        *sz = z.size;
+        *st = 0;
+    }
+    // pack (E2 / E3) into the zeroed output stage
+    __device__ __forceinline__ void emit(uint32_t excl, uint32_t sz,
+                                         uint32_t total)
+    {
+        QH_LDS u32x4 *o4 = (QH_LDS u32x4 *) wv->out;
+        const uint32_t n16 = (total + 15) / 16 + 1;
+        for (uint32_t i = lane_id(); i < n16; i += 64)
+            o4[i] = (u32x4){0, 0, 0, 0};
+        wave_sync();
+        if (sz)
+            emit_bits(wv->in, rs, re, mode, z.huff, z.plen, sm->enc, wv->out,
+                      excl);
+    }
+
+    __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
+                                              TileOffs to, Span sp, uint32_t sz,
+                                              uint32_t, uint8_t *out,
+                                              uint32_t *out_off, uint8_t *,
+                                              uint64_t n)
+    {
+        enc_slow_tile(in, mode, sm, wv, rs, re, z, c, t, cnt, to, sp, sz, out,
+                      out_off, n);
+    }
+};
+
+__global__ __launch_bounds__(64 * kWaves) void
 qhuff_encode_kernel(EncArgs a)
 {
     __shared__ EncSmem smem;
@@ -296,138 +552,18 @@ qhuff_encode_kernel(EncArgs a)
         clear_next_launch(a.c);
     }
     __syncthreads();                 // the only workgroup barrier
-
-    const uint32_t lane = lane_id();
-    QH_LDS EncWave *wv = &sm->w[tid >> 6];
-    QH_LDS uint32_t *stage = wv->in;
-    QH_LDS uint32_t *ostage = wv->out;
-    const QH_GLB uint32_t *gin_off = glb(a.in_off);
-    QH_GLB uint32_t *gout_off = glb(a.out_off);
-    const uint32_t n_waves = gridDim.x * kEncWaves;
-    const uint32_t gid = wave_gid(kEncWaves);
-    const uint32_t nt = a.c.n_tiles;
-    const uint32_t dbg = a.c.dbg;
-
-    auto tile_cnt = [&](uint32_t t) -> uint32_t {
-        return (uint32_t) min((uint64_t) kWT, a.n - (uint64_t) t * kWT);
-    };
-
-    // Tiles are claimed just in time: a wave claims its next tile only when
-    // it is about to code it, so claim order is processing order and a
-    // look-back only ever waits on tiles whose codec is already running.
-    // The claim -> offsets -> input latency of one wave hides under the
-    // codec work of the other waves on its SIMD.
-    PhaseClock clk;
-    clk.init(dbg);
-    for (;;)
-    {
-        const uint32_t t = claim_tile(a.c, gid, n_waves);
-        clk.lap(0);
-        if (t >= nt)
-            break;
-        const uint32_t cnt = tile_cnt(t);
-        TileOffs to;
-        to.load(gin_off, (uint64_t) t * kWT, cnt);
-        const Span sp = tile_span(a.in, to.first(), to.last(), kEncInCap);
-        if (sp.staged)
-        {
-            Chunks<kEncChunks> ch;
-            ch.load(sp);
-            ch.store<false>((QH_LDS u32x4 *) stage, sp.n16);
-        }
-        wave_sync();
-        clk.lap(1);
-
-        // 1. sizing (E1 / the framing choice of E3)
-        const bool valid = lane < cnt;
-        const uint32_t rs = valid ? (uint32_t) ((uintptr_t) (a.in + to.o0) - sp.pa) : 0;
-        const uint32_t re = valid ? (uint32_t) ((uintptr_t) (a.in + to.o1) - sp.pa) : 0;
-        EncSize z = {0, 0, true};
-        if (valid)
-            z = sp.staged ? size_string(a, EncLds{stage}, rs, re, sm->len)
-                          : size_string(a, EncGlb{(const QH_GLB uint32_t *) sp.pa},
-                                        rs, re, sm->len);
-        const uint32_t incl = wave_incl_scan(z.size);
-        const uint32_t excl = incl - z.size;
-        clk.lap(2);
-        const uint32_t total = read_lane(incl, 63);
-
-        // 2. publish the aggregate, issue the first look-back poll
-        LookBack lb;
-        if (!(dbg & kDbgNoLookback))
-            lb.start(a.c, t, total);
-        clk.lap(3);
-
-        // 3. pack (E2 / E3) into the zeroed output stage
-        const bool staged_out = total + 64 <= (uint32_t) kEncOutCap;
-        if (staged_out)
-        {
-            QH_LDS u32x4 *o4 = (QH_LDS u32x4 *) ostage;
-            const uint32_t n16 = (total + 16 + 15) / 16 + 1;
-            for (uint32_t i = lane; i < n16; i += 64)
-                o4[i] = (u32x4){0, 0, 0, 0};
-        }
-        wave_sync();
-        if (staged_out && valid && !(dbg & kDbgNoCodec))
-        {
-            Packer<PackLds> pk;
-            pk.sink.stage = ostage;
-            pk.init(16 + excl, 16 + excl + z.size);
-            if (sp.staged)
-                emit_string(EncLds{stage}, rs, re, a.mode, z.huff, z.plen,
-                            sm->enc, pk);
-            else
-                emit_string(EncGlb{(const QH_GLB uint32_t *) sp.pa}, rs, re,
-                            a.mode, z.huff, z.plen, sm->enc, pk);
-        }
-        wave_sync();
-
-        clk.lap(4);
-
-        // 4. output base
-        const uint64_t base = (dbg & kDbgNoLookback) ? (uint64_t) t << 13
-                            : lb.finish(a.c);
-        clk.lap(5);
-
-        // 5. copy-out
-        CopyOut<kEncOutChunks> co;
-        if (staged_out)
-            co.gather(ostage, a.out + base, total);
-        if (!(dbg & kDbgNoStore))
-        {
-            if (staged_out)
-                co.store();
-            else if (valid && !(dbg & kDbgNoCodec))
-            {
-                // output larger than the stage: pack straight to global
-                const uint32_t adj = (uint32_t) ((uintptr_t) a.out & 3);
-                Packer<PackGlb> pk;
-                pk.sink.out = a.out - adj;
-                const uint32_t p0 = adj + (uint32_t) base + excl;
-                pk.init(p0, p0 + z.size);
-                if (sp.staged)
-                    emit_string(EncLds{stage}, rs, re, a.mode, z.huff, z.plen,
-                                sm->enc, pk);
-                else
-                    emit_string(EncGlb{(const QH_GLB uint32_t *) sp.pa}, rs, re,
-                                a.mode, z.huff, z.plen, sm->enc, pk);
-            }
-            const uint64_t s0 = (uint64_t) t * kWT;
-            if (valid)
-                gout_off[s0 + lane] = (uint32_t) (base + excl);
-            if (t == nt - 1 && lane == 0)
-                gout_off[a.n] = (uint32_t) (base + total);
-        }
-        wave_sync();
-        clk.lap(6);
-    }
-    clk.flush(a.c.err);
+    EncPolicy pol;
+    pol.in = a.in;
+    pol.mode = a.mode;
+    pol.sm = sm;
+    pol.wv = &sm->w[tid >> 6];
+    tile_pipeline(pol, a.c, a.in, a.in_off, a.n, a.out, a.out_off, nullptr);
 }
 
 hipError_t
 launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st)
 {
-    hipLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(64 * kEncWaves),
+    hipLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(64 * kWaves),
                        0, st, a);
     return hipGetLastError();
 }
@@ -437,13 +573,13 @@ encode_occupancy(int *blocks_per_cu)
 {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
         blocks_per_cu, reinterpret_cast<const void *>(qhuff_encode_kernel),
-        64 * kEncWaves, 0);
+        64 * kWaves, 0);
 }
 
 int
 encode_waves_per_block()
 {
-    return kEncWaves;
+    return kWaves;
 }
 
 size_t

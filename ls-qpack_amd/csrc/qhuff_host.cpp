@@ -40,8 +40,9 @@ struct qhuff_ctx
     uint32_t *err;                       // device: [0] error word, [1..3]
                                          // census, then claim counters
     uint64_t cap_tiles, cap_super;
+    unsigned long long *prof;            // QHUFF_PROFILE builds: stamp buffer
+    size_t prof_words;
     uint32_t epoch;
-    uint32_t dbg;                        // QHUFF_DEBUG ablation switches
     // host-path staging
     uint8_t *h_stage;                    // pinned
     size_t h_stage_cap;
@@ -50,8 +51,8 @@ struct qhuff_ctx
     char err_msg[256];
 };
 
-// device words: [0] error, then the claim counters
-constexpr size_t kErrWords = kCtrStride * (1 + 2 * kGroups);
+// device words: [0] sticky error word (rest reserved)
+constexpr size_t kErrWords = 64;
 
 static int
 fail(qhuff_ctx *c, hipError_t e, const char *what)
@@ -109,9 +110,9 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         delete c;
         return rc ? rc : QHUFF_EDEVICE;
     }
-    // Every wave claims tiles until the batch is done (claims never wait on
-    // an unstarted wave, so the grid need not be co-resident): one full
-    // round of resident workgroups.
+    // Tiles are assigned statically to the waves of the grid and a
+    // look-back may wait on any earlier tile, so the grid must be
+    // co-resident: at most the workgroups that fit at once.
     c->enc_grid = (uint32_t) (occ_e * c->n_cu);
     c->dec_grid = (uint32_t) (occ_d * c->n_cu);
     e = hipMalloc((void **) &c->tab, sizeof(DevTables));
@@ -136,17 +137,16 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     }
     c->epoch = 0;
     {
-        const char *d = getenv("QHUFF_DEBUG");
-        c->dbg = d ? (uint32_t) strtoul(d, nullptr, 0) : 0;
-        const char *g = getenv("QHUFF_GRID_WG_PER_CU");  // tuning override
+        // tuning override: fewer workgroups per CU than fit (never more: the
+        // look-back needs the whole grid co-resident)
+        const char *g = getenv("QHUFF_GRID_WG_PER_CU");
         if (g)
         {
             uint32_t k = (uint32_t) strtoul(g, nullptr, 0);
-            if (k >= 1)
-            {
+            if (k >= 1 && k <= (uint32_t) occ_e)
                 c->enc_grid = k * c->n_cu;
+            if (k >= 1 && k <= (uint32_t) occ_d)
                 c->dec_grid = k * c->n_cu;
-            }
         }
     }
     *ctx_out = c;
@@ -172,6 +172,8 @@ qhuff_close(qhuff_ctx *c)
         (void) hipFree(c->d_stage);
     if (c->h_stage)
         (void) hipHostFree(c->h_stage);
+    if (c->prof)
+        (void) hipFree(c->prof);
     if (c->own_stream)
         (void) hipStreamDestroy(c->own_stream);
     delete c;
@@ -197,16 +199,18 @@ qhuff_device_error(qhuff_ctx *c)
     return (int) v;
 }
 
-extern "C" int
-qhuff_debug_clock(qhuff_ctx *c, uint64_t *out, uint32_t n)
+// Profile builds: copy the stamp buffer of the last launch (synchronous).
+// Returns the number of u64 words available (0 in normal builds).
+extern "C" uint64_t
+qhuff_profile_read(qhuff_ctx *c, uint64_t *dst, uint64_t max_words)
 {
-    if (!c || !out || n > (uint32_t) kPhases)
-        return QHUFF_EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipDeviceSynchronize());
-    HIPCHK(c, hipMemcpy(out, c->err + 16, 8 * n, hipMemcpyDeviceToHost));
-    HIPCHK(c, hipMemset(c->err + 16, 0, 8 * kPhases));
-    return QHUFF_OK;
+    if (!c || !c->prof)
+        return 0;
+    (void) hipDeviceSynchronize();
+    const uint64_t w = c->prof_words < max_words ? c->prof_words : max_words;
+    if (dst && w)
+        (void) hipMemcpy(dst, c->prof, w * 8, hipMemcpyDeviceToHost);
+    return c->prof_words;
 }
 
 extern "C" uint64_t
@@ -257,12 +261,10 @@ prepare_launch(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
     c->epoch = (c->epoch + 1) & kEpochMask;
     if (c->epoch == 0)
     {
-        // wrapped: stale flags could alias the new epoch, and the counters
-        // of epoch 1 were last used, not cleared
+        // wrapped: stale flags could alias the new epoch, and the
+        // accumulators of epoch 1 were last used, not cleared
         HIPCHK(c, hipMemsetAsync(c->flags, 0, lb_bytes(c->cap_tiles, c->cap_super),
                                  st));
-        HIPCHK(c, hipMemsetAsync(c->err + kCtrStride, 0,
-                                 2 * kGroups * kCtrStride * sizeof(uint32_t), st));
         c->epoch = 1;
     }
     return QHUFF_OK;
@@ -272,15 +274,24 @@ static Coord
 coord(qhuff_ctx *c, uint64_t tiles)
 {
     Coord k;
+    k.prof = nullptr;
+#ifdef QHUFF_PROFILE
+    {
+        const size_t words = (size_t) c->n_cu * 32 * kProfIters * kProfSlots;
+        if (!c->prof && hipMalloc((void **) &c->prof, words * 8) == hipSuccess)
+            c->prof_words = words;
+        if (c->prof)
+            (void) hipMemset(c->prof, 0, c->prof_words * 8);
+        k.prof = c->prof;
+    }
+#endif
     k.flags = c->flags;
     k.sflags = c->flags + c->cap_tiles;
     k.sacc = k.sflags + c->cap_super;
     k.cap_super = (uint32_t) c->cap_super;
     k.err = c->err;
-    k.ctr = c->err + kCtrStride;
     k.epoch = c->epoch;
     k.n_tiles = (uint32_t) tiles;
-    k.dbg = c->dbg;
     return k;
 }
 

@@ -1,0 +1,227 @@
+// qhuff_pipeline.h -- the per-wave tile loop shared by the encode and decode
+// kernels (see qhuff_device.h for the execution model).
+//
+// Wave g codes tiles g, g + W, g + 2W, ... (W = waves in the grid; the grid
+// is at most what is co-resident, so every tile a look-back waits on belongs
+// to a running wave).  Per iteration, for tile t (input already in the LDS
+// stage):
+//
+//   top    one wait for everything the last iteration issued (issued about
+//          a codec ago, so it has landed); the previous tile's super-
+//          accumulator add has returned: if it completed its super tile,
+//          publish the super aggregate; write t's input (loaded last
+//          iteration) into the stage; load the next tile's input and the
+//          offsets of the one after it; poll the previous tile's look-back
+//          windows
+//   codec  P::codec() -- LDS only -- per-lane output size (+ status)
+//   scan   wave scan -> tile-local offsets, tile total; publish the tile
+//          aggregate and add it to the super accumulator (LookBack::start)
+//   defer  resolve the look-back of the tile coded TWO iterations ago (its
+//          polls were issued at the top, a codec ago) and store its output
+//          (parked in the wave's LDS hold buffer), offsets and status; park
+//          the previous tile's output (registers) in the hold buffer
+//   emit   P::emit() -- compacted output of t into the LDS out stage --
+//          gathered into registers (TileOut), to be stored next iteration
+//
+// Tiles whose input or output does not fit the stages are coded eagerly by
+// P::slow_tile() (out of line) after the deferred tile has been flushed.
+#pragma once
+
+#include "qhuff_kernels.h"
+
+namespace qhuff {
+
+constexpr int kChunks = 3;                  // 16-byte input chunks per lane
+constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: input / output stage
+
+// A coded tile waiting for its look-back: per-lane output offset and status,
+// the look-back state.  Its output bytes wait in registers (the newer of the
+// two deferred tiles) or in the wave's LDS hold buffer (the older).
+struct Pending
+{
+    bool valid;
+    uint32_t tile, cnt, total;
+    uint32_t excl;                   // this lane's tile-local output offset
+    uint32_t stat;                   // this lane's status byte
+    LookBack lb;
+};
+
+// resolve a pending tile's base and store it from `o` (every lane)
+template <bool kStatus>
+__device__ __forceinline__ void
+flush_tile(const Coord &c, Pending &d, const TileOut<kChunks> &o, uint8_t *out,
+           uint32_t *out_off, uint8_t *status, uint64_t n, uint32_t it = ~0u)
+{
+    const uint64_t base = d.lb.finish(c);
+    prof_stamp(c, it, 7);
+    prof_value(c, it, 8, d.lb.spins_seen);
+    o.store(out + base, d.total);
+    const uint32_t lane = lane_id();
+    const uint64_t s0 = (uint64_t) d.tile * kWT;
+    if (lane < d.cnt)
+    {
+        ((QH_GLB uint32_t *) out_off)[s0 + lane] = (uint32_t) (base + d.excl);
+        if (kStatus)
+            ((QH_GLB uint8_t *) status)[s0 + lane] = (uint8_t) d.stat;
+    }
+    if (d.tile == c.n_tiles - 1 && lane == 0)
+        ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + d.total);
+    d.valid = false;
+}
+
+// the older pending tile, output from the hold buffer
+template <bool kStatus>
+__device__ __forceinline__ void
+flush_held(const Coord &c, Pending &d, QH_LDS uint32_t *hold,
+           uint8_t *out, uint32_t *out_off, uint8_t *status, uint64_t n,
+           uint32_t it = ~0u)
+{
+    TileOut<kChunks> o;
+    o.gather(hold);
+    flush_tile<kStatus>(c, d, o, out, out_off, status, n, it);
+}
+
+// vmcnt(0), other counters untouched (gfx9 s_waitcnt encoding)
+__device__ __forceinline__ void
+wait_vm_all()
+{
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+}
+
+template <class P>
+__device__ __forceinline__ void
+tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_p,
+              uint64_t n, uint8_t *out, uint32_t *out_off, uint8_t *status)
+{
+    const QH_GLB uint32_t *in_off = (const QH_GLB uint32_t *) in_off_p;
+    const uint32_t lane = lane_id();
+    const uint32_t W = gridDim.x * kWaves;
+    const uint32_t nt = c.n_tiles;
+    uint32_t t = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (t >= nt)
+        return;
+    auto cnt_of = [&](uint32_t tt) -> uint32_t {
+        return (uint32_t) min((uint64_t) kWT, n - (uint64_t) tt * kWT);
+    };
+    // the tile loads for tile ids past the end read the last tile instead
+    // (fixed instruction counts; the data is never used)
+    auto clamp = [&](uint64_t tt) -> uint32_t {
+        return tt < nt ? (uint32_t) tt : nt - 1;
+    };
+
+    // prologue: offsets of t and t + W, input of t (landed at the top)
+    TileOffs o_cur, o_nxt, o_nn;
+    o_cur.load(in_off, (uint64_t) t * kWT, cnt_of(t));
+    const uint32_t tn = clamp((uint64_t) t + W);
+    o_nxt.load(in_off, (uint64_t) tn * kWT, cnt_of(tn));
+    Span sp_cur = tile_span(in, o_cur.first(), o_cur.last(), kStageCap);
+    Chunks<kChunks> ch;
+    ch.load(sp_cur);
+
+    // Two tiles are pending at a time.  Tile k's look-back is resolved at
+    // the top of iteration k + 2; its windows are polled at the end of
+    // iteration k + 1, a whole codec after every tile before it published
+    // its aggregate (waves start staggered by the dispatch, and a round's
+    // first tiles wait on the previous round's last ones).  Between its
+    // codec and the top of the next iteration a tile's output sits in
+    // registers; then it is parked in the wave's LDS hold buffer -- so no
+    // large register set is live across a codec.
+    Pending older, newer;
+    older.valid = newer.valid = false;
+    TileOut<kChunks> newer_out;
+    QH_LDS uint32_t *hold = pol.hold();
+    uint32_t it = 0;
+    for (uint64_t tile_k = t;; ++it)
+    {
+        prof_stamp(c, it, 0);
+        // top: one wait for everything the last iteration issued -- the
+        // input of t, offsets, the held tile's polls, the newer tile's
+        // super-accumulator add, the stores of the tile before
+        wait_vm_all();
+        prof_stamp(c, it, 1);
+        if (newer.valid)
+            newer.lb.super_agg(c);
+        if (older.valid)
+            flush_held<P::kStatus>(c, older, hold, out, out_off, status, n,
+                                   it);
+        wave_sync();
+        if (newer.valid)
+            newer_out.park(hold);
+        older = newer;
+        newer.valid = false;
+        if (sp_cur.staged)
+            pol.stage_in(ch, sp_cur);
+        wave_sync();
+        prof_stamp(c, it, 2);
+
+        // codec of t (LDS only when staged)
+        const uint32_t cnt = cnt_of(t);
+        uint32_t sz = 0, st = 0;
+        bool fast = sp_cur.staged;
+        if (fast)
+            pol.codec(o_cur, cnt, sp_cur, &sz, &st);
+        const uint32_t incl = wave_incl_scan(sz);
+        const uint32_t excl = incl - sz;
+        const uint32_t total = read_lane(incl, 63);
+        fast = fast && total + 64 <= (uint32_t) kStageCap;
+        prof_stamp(c, it, 3);
+
+        // loads for the next tile
+        const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), kStageCap);
+        ch.load(sp_nxt);
+        const uint32_t tz = clamp(tile_k + 2ull * W);
+        o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
+
+        if (fast)
+        {
+            newer.valid = true;
+            newer.tile = t;
+            newer.cnt = cnt;
+            newer.total = total;
+            newer.excl = excl;
+            newer.stat = st;
+            newer.lb.start(c, t, total);
+            prof_stamp(c, it, 4);
+            wave_sync();
+            pol.emit(excl, sz, total);
+            wave_sync();
+            prof_stamp(c, it, 9);
+            newer_out.gather(pol.out_stage());
+        }
+        else
+        {
+            if (older.valid)
+            {
+                older.lb.poll(c);
+                flush_held<P::kStatus>(c, older, hold, out, out_off, status, n);
+            }
+            pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
+                          status, n);
+        }
+        if (older.valid)
+            older.lb.poll(c);
+        prof_stamp(c, it, 5);
+        wave_sync();
+        prof_stamp(c, it, 6);
+
+        tile_k += W;
+        if (tile_k >= nt)
+            break;
+        o_cur = o_nxt;
+        o_nxt = o_nn;
+        t = (uint32_t) tile_k;
+        sp_cur = sp_nxt;
+    }
+    wait_vm_all();
+    if (newer.valid)
+        newer.lb.super_agg(c);
+    if (older.valid)
+        flush_held<P::kStatus>(c, older, hold, out, out_off, status, n);
+    if (newer.valid)
+    {
+        newer.lb.poll(c);
+        flush_tile<P::kStatus>(c, newer, newer_out, out, out_off, status, n);
+    }
+}
+
+}  // namespace qhuff

@@ -25,7 +25,7 @@ EXPORTS = (
     "qhuff_encode_batch", "qhuff_decode_batch", "qhuff_encode_batch_host",
     "qhuff_decode_batch_host", "qhuff_enc_enc_str", "qhuff_enc_str_size",
     "qhuff_huff_decode", "qhuff_last_error", "qhuff_shard_cuts",
-    "qhuff_synth_batch", "qhuff_device_error", "qhuff_debug_clock",
+    "qhuff_synth_batch", "qhuff_device_error", "qhuff_profile_read",
 )
 
 
@@ -71,8 +71,8 @@ def lib():
         L.qhuff_enc_enc_str.restype = C.c_int
         L.qhuff_enc_enc_str.argtypes = [vp, C.c_uint, vp, C.c_size_t,
                                         C.c_char_p, C.c_uint]
-        L.qhuff_debug_clock.restype = C.c_int
-        L.qhuff_debug_clock.argtypes = [vp, vp, C.c_uint32]
+        L.qhuff_profile_read.restype = C.c_uint64
+        L.qhuff_profile_read.argtypes = [vp, vp, C.c_uint64]
         L.qhuff_enc_str_size.restype = C.c_uint
         L.qhuff_enc_str_size.argtypes = [vp, C.c_char_p, C.c_uint]
         L.qhuff_huff_decode.restype = DecodeRetval
@@ -158,11 +158,16 @@ class Codec:
         except Exception:
             pass
 
-    def debug_clock(self):
-        """Per-phase cycle sums of QHUFF_DEBUG=0x40 launches (then cleared)."""
-        v = (C.c_uint64 * 8)()
-        self._check(lib().qhuff_debug_clock(self._ctx, v, 8), "qhuff_debug_clock")
-        return list(v)
+    def profile_read(self):
+        """Phase stamps of the last launch (QHUFF_PROFILE build), as a
+        numpy uint64 array, or None in a normal build."""
+        import numpy as np
+        n = lib().qhuff_profile_read(self._ctx, None, 0)
+        if not n:
+            return None
+        a = np.zeros(n, dtype=np.uint64)
+        lib().qhuff_profile_read(self._ctx, a.ctypes.data, n)
+        return a
 
     def device_error(self):
         """Synchronise and return (then clear) the sticky device error word

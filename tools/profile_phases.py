@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Per-phase cycle breakdown of the wave pipeline from a QHUFF_PROFILE build
+(make -C ls-qpack_amd prof; run with QHUFF_LIB=.../libqhuff_prof.so).
+Slots per wave iteration (qhuff_pipeline.h): 0 top, 1 after the drain,
+2 after stage + loads + polls, 3 after codec + scan, 4 after lb.start,
+5 after the deferred flush, 6 end of iteration."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ls-qpack_amd"))
+os.environ.setdefault("QHUFF_LIB", os.path.join(ROOT, "ls-qpack_amd",
+                                                "libqhuff_prof.so"))
+
+import numpy as np
+import torch
+import qhuff
+
+ITERS, SLOTS = 16, 10
+NAMES = ["drain", "flush+park+stage", "codec+scan", "loads+lb.start",
+         "emit+gather+poll", "end"]
+
+
+def report(tag, p):
+    p = p.reshape(-1, ITERS, SLOTS).astype(np.int64)
+    live = p[:, :, 0] != 0
+    waves = int(live[:, 0].sum())
+    t0 = p[live[:, 0], 0, 0].min()
+    print("%s: %d waves, iterations/wave %.2f" % (tag, waves,
+                                                  live.sum() / max(waves, 1)))
+    for ph in range(6):
+        a, b = p[:, :, ph], p[:, :, ph + 1]
+        ok = live & (a != 0) & (b != 0)
+        d = (b - a)[ok]
+        if d.size:
+            print("  %-12s mean %8.0f  p50 %8.0f  p90 %8.0f  max %8.0f cyc"
+                  % (NAMES[ph], d.mean(), np.median(d), np.percentile(d, 90),
+                     d.max()))
+    ok = live & (p[:, :, 1] != 0) & (p[:, :, 7] != 0)
+    if ok.any():
+        lbt = (p[:, :, 7] - p[:, :, 1])[ok]
+        stt = (p[:, :, 2] - p[:, :, 7])[ok]
+        sp = p[:, :, 8][ok]
+        print("  flush: look-back mean %.0f p90 %.0f | stores+park+stage mean %.0f | re-polls mean %.2f, >0 in %.1f%%, max %d"
+              % (lbt.mean(), np.percentile(lbt, 90), stt.mean(), sp.mean(),
+                 100.0 * (sp > 0).mean(), sp.max()))
+    ok = live & (p[:, :, 4] != 0) & (p[:, :, 9] != 0)
+    if ok.any():
+        a = (p[:, :, 9] - p[:, :, 4])[ok]
+        b = (p[:, :, 5] - p[:, :, 9])[ok]
+        print("  emit: emit mean %.0f p90 %.0f | gather+poll mean %.0f p90 %.0f"
+              % (a.mean(), np.percentile(a, 90), b.mean(), np.percentile(b, 90)))
+    return
+    # timeline: start of iterations relative to the first stamp
+    for it in range(0, ITERS):
+        ok = live[:, it]
+        if not ok.any():
+            break
+        s = p[ok, it, 0] - t0
+        e = p[ok, it, 6] - t0
+        e = e[p[ok, it, 6] != 0]
+        print("  iter %2d: waves %5d  start p50 %8.0f max %8.0f   end p50 %8.0f max %8.0f"
+              % (it, ok.sum(), np.median(s), s.max(),
+                 np.median(e) if e.size else 0, e.max() if e.size else 0))
+
+
+def main():
+    n = int(os.environ.get("N", 1 << 20))
+    data, off = qhuff.synth_batch(n)
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(off.view(np.int32)).to(dev)
+    codec = qhuff.Codec(0)
+    for _ in range(3):
+        h, ho = codec.encode(d, o, 0)
+    torch.cuda.synchronize()
+    report("encode", codec.profile_read())
+    hb = int(ho[-1].item())
+    h = h[:hb].clone()
+    for _ in range(3):
+        codec.decode(h, ho)
+    torch.cuda.synchronize()
+    report("decode", codec.profile_read())
+    codec.close()
+
+
+if __name__ == "__main__":
+    main()
