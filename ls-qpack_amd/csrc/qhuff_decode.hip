@@ -26,6 +26,13 @@
 // tile's output base.
 #include "qhuff_pipeline.h"
 
+// 1: decoded bytes go to the arena as one unaligned 2-byte store per step
+// instead of two byte stores -- measured 45% slower on MI355X (unaligned LDS
+// stores are split), kept off
+#ifndef QH_EMIT_B16
+#define QH_EMIT_B16 0
+#endif
+
 namespace qhuff {
 
 constexpr int kDecInCap = kStageCap;                   // staged input bytes
@@ -38,7 +45,6 @@ struct DecWave                       // one wave's private LDS region
 {
     alignas(16) uint32_t in[kDecInCap / 4];   // BE input dwords; output stage
     alignas(16) uint8_t arena[kArenaBytes];
-    alignas(16) uint32_t hold[kStageCap / 4];  // the older pending tile's output
 };
 
 struct DecSmem
@@ -294,7 +300,8 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         buf |= (uint64_t) dd << ((32 - bits) & 31);
         bits += need ? 32u : 0u;
         p += need ? 1u : 0u;
-        nx = src[p];
+        if (need)
+            nx = src[p];
     } while (__builtin_amdgcn_ballot_w64(rem >= 32));
 
     // epilogue: the last < 32 bits, padded with ones; D3 tail rule
@@ -345,8 +352,13 @@ struct ArenaEmit
     uint32_t n;
     __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
     {
+#if QH_EMIT_B16
+        // one 2-byte store at any byte address (LDS unaligned access)
+        *(QH_LDS uint16_t *) (slot + n) = (uint16_t) val;
+#else
         slot[n] = (uint8_t) val;
         slot[n + 1] = (uint8_t) (val >> 8);
+#endif
         n += nb;
     }
 };
@@ -460,17 +472,13 @@ struct DecPolicy
     uint32_t slot0;                  // this lane's arena slot (current tile)
 
     __device__ __forceinline__ void stage_in(const Chunks<kChunks> &ch,
-                                             const Span &sp)
+                                             const Span &sp, const TileOffs &)
     {
         ch.store<true>((QH_LDS u32x4 *) wv->in, sp.n16);
     }
     __device__ __forceinline__ const QH_LDS uint32_t *out_stage() const
     {
         return wv->in;
-    }
-    __device__ __forceinline__ QH_LDS uint32_t *hold() const
-    {
-        return wv->hold;
     }
     // staged tile: decode this lane's string into its arena slot
     __device__ __forceinline__ void codec(const TileOffs &to, uint32_t cnt,

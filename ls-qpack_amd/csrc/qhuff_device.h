@@ -28,7 +28,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWT = 64;                     // strings per wave tile
-constexpr int kWaves = 12;                  // waves per workgroup (both kernels)
+#ifndef QH_WAVES
+#define QH_WAVES 12
+#endif
+constexpr int kWaves = QH_WAVES;            // waves per workgroup (per kernel TU)
 
 // Look-back flag word: [63:42] launch epoch, [41:40] state (1 aggregate,
 // 2 inclusive), [39:0] byte count.  Epoch on top: within a launch an
@@ -102,18 +105,29 @@ wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// wave inclusive scan of one uint32 per lane
+// DPP move of v (gfx9 dpp_ctrl CTRL on rows ROWS); lanes whose source lies
+// outside the pattern, or whose row is masked off, read 0
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t
+dpp0(uint32_t v)
+{
+    return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, CTRL, ROWS, 0xf,
+                                                  false);
+}
+
+// wave inclusive scan of one uint32 per lane: scans of the four 16-lane rows
+// by row shifts, then the row totals broadcast down (row_bcast:15 / 31) --
+// VALU only, no LDS traffic
 __device__ __forceinline__ uint32_t
 wave_incl_scan(uint32_t v)
 {
-    const uint32_t lane = lane_id();
     uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1)
-    {
-        const uint32_t y = __shfl_up(x, d, 64);
-        x += lane >= (uint32_t) d ? y : 0u;
-    }
+    x += dpp0<0x111, 0xf>(x);                 // row_shr:1
+    x += dpp0<0x112, 0xf>(x);                 // row_shr:2
+    x += dpp0<0x114, 0xf>(x);                 // row_shr:4
+    x += dpp0<0x118, 0xf>(x);                 // row_shr:8
+    x += dpp0<0x142, 0xa>(x);                 // row_bcast:15 -> rows 1, 3
+    x += dpp0<0x143, 0xc>(x);                 // row_bcast:31 -> rows 2, 3
     return x;
 }
 

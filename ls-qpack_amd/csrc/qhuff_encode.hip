@@ -1,42 +1,57 @@
 // qhuff_encode.hip -- batch Huffman encode kernel (gfx950).
 //
 // Reference path:
-//   E1 qenc_enc_str_size   lsqpack.c:5198-5210  -> sizing pass below
-//   E2 qenc_huffman_enc    lsqpack.c:5085-5195  -> packing pass below
+//   E1 qenc_enc_str_size   lsqpack.c:5198-5210  -> sizing
+//   E2 qenc_huffman_enc    lsqpack.c:5085-5195  -> packing
 //   E3 lsqpack_enc_enc_str lsqpack.c:839-876    -> LITERAL modes (H bit,
 //                          prefixed length, strict-< Huffman-vs-raw choice)
 //
-// One string per lane, one 64-string tile per wave (qhuff_device.h).  Per
-// tile:
-//   1. the tile's packed input bytes sit in the wave's LDS input stage
-//      (coalesced 16-B loads issued one tile ahead);
-//   2. sizing pass per lane (code-length sum out of an LDS table), the
-//      Huffman-or-raw choice of the literal modes;
-//   3. wave scan -> tile-local output offsets; aggregate published and the
-//      first look-back window polled at once;
-//   4. packing pass per lane into the zeroed LDS output stage (MSB-first bit
-//      accumulator, big-endian words, EOS-prefix padding);
-//   5. look-back for the tile's global output base; shifted copy-out with
-//      16-byte aligned global stores; out_off stores.
-// Tiles whose input or output does not fit the LDS stages take the same
-// steps with global reads / per-lane global writes (correct, slower).
+// One 64-string tile per wave (qhuff_device.h, qhuff_pipeline.h).  The
+// tile's packed input arrives as 16-byte chunks in registers (lane l holds
+// chunks l, l + 64, l + 128 of the tile's 16-byte aligned span).  Per tile:
+//   1. dense pass, byte-parallel (no per-string work, no divergence): each
+//      lane looks up the codes of its 16 bytes per row (one LDS read per
+//      byte), the row's lane sums are scanned across the wave, and the codes
+//      are OR-ed four at a time into a dense bit stream -- the codes of every
+//      byte of the span back to back, with no padding or framing.  Each
+//      byte's code length (u8) and each chunk's dense offset stay in LDS;
+//   2. sizing, string per lane: a string's Huffman bits (E1) are the
+//      difference of the dense offsets of its two ends -- a chunk offset
+//      plus a SAD over at most 16 byte lengths each; the E3 choice; wave
+//      scan -> tile-local output offsets;
+//   3. emit, string per lane: framing bits, the string's range of the dense
+//      stream funnel-copied word by word to its byte-aligned output position,
+//      EOS-prefix padding (lsqpack.c:5171-5189); raw strings copied from the
+//      staged input;
+//   4. look-back for the tile's global output base, 16-byte stores
+//      (qhuff_pipeline.h).
+// A tile holding a code longer than 15 bits (control and high bytes) or
+// whose dense stream overflows is sized and packed string per lane from the
+// staged input instead; tiles that do not fit the stages take the slow path
+// (global reads / per-lane global writes).
 #include "qhuff_pipeline.h"
 
 namespace qhuff {
 
 constexpr int kEncInCap = kStageCap;          // staged input bytes per tile
 constexpr int kEncOutCap = kStageCap;         // output stage bytes per tile
+constexpr int kDenseWords = kStageCap / 4 + 4;  // dense code stream (words)
+constexpr uint32_t kDenseBits = 32u * (kDenseWords - 2);
+constexpr int kSpanChunks = kStageCap / 16;   // 16-byte chunks per staged span
 
 struct EncWave                                // one wave's private LDS region
 {
     alignas(16) uint32_t in[kEncInCap / 4 + 4];
-    alignas(16) uint32_t out[kEncOutCap / 4];
-    alignas(16) uint32_t hold[kStageCap / 4];  // the older pending tile's output
+    alignas(16) uint32_t dense[kDenseWords];    // codes back to back, MSB first
+    alignas(16) uint32_t out[kEncOutCap / 4];   // byte code lengths until emit
+    uint32_t s0[kSpanChunks];                   // dense offset of each chunk
 };
 
 struct EncSmem
 {
     u32x2 enc[257];
+    uint32_t mt[256];                // dense pass: code | len << 27 (len <= 15),
+                                     // 31 << 27 for longer codes
     uint8_t len[256];
     EncWave w[kWaves];
 };
@@ -53,25 +68,10 @@ struct EncGlb
     __device__ __forceinline__ uint32_t dw(uint32_t i) const { return w[i]; }
 };
 
-// MSB-first bit packer.  Words are flushed as big-endian dwords at 4-byte
-// aligned positions; `lo`..`hi` are the bytes this string owns.
-struct PackLds                               // into a zeroed LDS stage
-{
-    QH_LDS uint32_t *stage;
-    // a dword this string owns whole is stored; one it shares with a
-    // neighbour (its first / last) is OR-ed in
-    __device__ __forceinline__ void word(uint32_t wpos, uint32_t be,
-                                         uint32_t lo, uint32_t hi) const
-    {
-        if (wpos >= lo && wpos + 4 <= hi)
-            stage[wpos >> 2] = bswap32(be);
-        else
-            __hip_atomic_fetch_or(&stage[wpos >> 2], bswap32(be),
-                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-};
-
-struct PackGlb                               // direct global stores
+// MSB-first bit packer writing straight to global memory (slow path).
+// Words are flushed as big-endian dwords at 4-byte aligned positions;
+// `lo`..`hi` are the bytes this string owns.
+struct PackGlb
 {
     uint8_t *out;                            // 4-byte aligned
     __device__ __forceinline__ void word(uint32_t wpos, uint32_t be,
@@ -178,8 +178,8 @@ len4(uint32_t w, const QH_LDS uint8_t *s_len)
 }
 
 // sum of code lengths over bytes [rs, re) (positions relative to the source):
-// two dwords per iteration (independent LDS lookups in flight together),
-// four lengths packed per dword, masked and summed with v_sad_u8
+// two dwords per iteration, four lengths packed per dword, masked and summed
+// with v_sad_u8
 template <class Src>
 __device__ __forceinline__ uint32_t
 code_bits(const Src &src, uint32_t rs, uint32_t re, const QH_LDS uint8_t *s_len)
@@ -214,13 +214,12 @@ pack_string(const Src &src, uint32_t rs, uint32_t re, bool raw,
     {
         const uint32_t w = src.dw(d);
         const uint32_t m = byte_mask(d, d0, dl, rs, re);
-        // unconditional lookups (independent LDS reads), then masked puts
         u32x2 e[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b)
         {
             const uint32_t c = (w >> (8 * b)) & 0xff;
-            const u32x2 t = s_enc[c];            // always read: no branch
+            const u32x2 t = s_enc[c];
             e[b].x = raw ? c : t.x;
             e[b].y = raw ? 8u : t.y;
         }
@@ -230,13 +229,11 @@ pack_string(const Src &src, uint32_t rs, uint32_t re, bool raw,
     }
 }
 
-// ---- branch-free packing into the LDS stage ------------------------------
+// ---- bit packing into an LDS output stage --------------------------------
 //
-// The stage holds the tile's output as a big-endian bit stream in dwords
-// (byte-swapped words), zeroed before packing.  Every code is OR-ed in at its
-// bit position: the only loop-carried state is the position, there is no
-// data-dependent flush, and neighbouring strings (which share boundary
-// dwords) need no coordination.
+// The stage holds the tile's output in byte order (byte-swapped big-endian
+// words), zeroed before packing; bits are OR-ed in at their positions, so
+// neighbouring strings (which share boundary words) need no coordination.
 
 // OR the `len` (<= 32) low bits of v into the stream at bit `pos`
 __device__ __forceinline__ void
@@ -251,11 +248,6 @@ or_bits(QH_LDS uint32_t *st, uint32_t pos, uint32_t v, uint32_t len)
                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// E2 / E3 payload of bytes [rs, re) of the LDS input, from bit `pos`; four
-// input bytes per step: their codes are concatenated (at most 32 bits in the
-// common case -- every code of <= 8 bits, and raw bytes) and OR-ed in with
-// one two-dword OR; a wave-uniform branch takes any step with a longer
-// concatenation code by code.  Returns the end position.
 // codes of the (masked) bytes of one input dword
 __device__ __forceinline__ void
 codes4(uint32_t w, uint32_t m, bool raw, const QH_LDS u32x2 *s_enc,
@@ -283,6 +275,10 @@ cat4(const uint32_t (&c)[4], const uint32_t (&l)[4])
     return v;
 }
 
+// E2 / E3 payload of bytes [rs, re) of the LDS input (string per lane), from
+// bit `pos`; four input bytes per step, their codes concatenated and OR-ed
+// in at once when they fit 32 bits (a wave-uniform branch takes the others
+// code by code).  Returns the end position.
 __device__ __forceinline__ uint32_t
 pack_bits(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, bool raw,
           const QH_LDS u32x2 *s_enc, QH_LDS uint32_t *st, uint32_t pos)
@@ -327,8 +323,34 @@ pack_bits(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, bool raw,
     return pos;
 }
 
+// literal framing (lsqpack.c:852-854, 862-864, 819-836): H bit + the length
+// as an HPACK integer with a `mode`-bit prefix, at bit `pos`; returns the
+// position after it
+__device__ __forceinline__ uint32_t
+emit_prefix(QH_LDS uint32_t *st, uint32_t pos, uint32_t mode, bool huff,
+            uint32_t plen)
+{
+    const uint32_t mask = (1u << mode) - 1, first = huff ? (1u << mode) : 0;
+    if (plen < mask)
+    {
+        or_bits(st, pos, first | plen, 8);
+        return pos + 8;
+    }
+    or_bits(st, pos, first | mask, 8);
+    pos += 8;
+    uint32_t v = plen - mask;
+    while (v >= 128)
+    {
+        or_bits(st, pos, 0x80 | (v & 0x7f), 8);
+        pos += 8;
+        v >>= 7;
+    }
+    or_bits(st, pos, v, 8);
+    return pos + 8;
+}
+
 // literal framing + payload + EOS-prefix padding into the LDS stage, from
-// byte `start` (lsqpack.c:839-876, 5171-5189)
+// byte `start`, string per lane (lsqpack.c:839-876, 5171-5189)
 __device__ __forceinline__ void
 emit_bits(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
           bool huff, uint32_t plen, const QH_LDS u32x2 *s_enc,
@@ -336,28 +358,7 @@ emit_bits(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
 {
     uint32_t pos = 8 * start;
     if (mode)
-    {
-        const uint32_t mask = (1u << mode) - 1, first = huff ? (1u << mode) : 0;
-        if (plen < mask)
-        {
-            or_bits(st, pos, first | plen, 8);
-            pos += 8;
-        }
-        else
-        {
-            or_bits(st, pos, first | mask, 8);
-            pos += 8;
-            uint32_t v = plen - mask;
-            while (v >= 128)
-            {
-                or_bits(st, pos, 0x80 | (v & 0x7f), 8);
-                pos += 8;
-                v >>= 7;
-            }
-            or_bits(st, pos, v, 8);
-            pos += 8;
-        }
-    }
+        pos = emit_prefix(st, pos, mode, huff, plen);
     pos = pack_bits(in, rs, re, !huff, s_enc, st, pos);
     const uint32_t pad = (8 - (pos & 7)) & 7;
     if (pad)
@@ -365,7 +366,7 @@ emit_bits(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
 }
 
 // literal framing (lsqpack.c:852-854, 862-864, 819-836): H bit + prefixed
-// length, then the payload
+// length, then the payload (slow path, straight to global memory)
 template <class Src, class Sink>
 __device__ __forceinline__ void
 emit_string(const Src &src, uint32_t rs, uint32_t re, uint32_t mode,
@@ -400,27 +401,217 @@ struct EncSize
     bool huff;
 };
 
-template <class Src>
+// E1 bits -> output size and the E3 choice (strict <, lsqpack.c:848)
 __device__ __forceinline__ EncSize
-size_string(uint32_t mode, const Src &src, uint32_t rs, uint32_t re,
-            const QH_LDS uint8_t *s_len)
+size_from_bits(uint32_t mode, uint32_t bits, uint32_t len)
 {
     EncSize z;
-    const uint32_t len = re - rs;
-    const uint32_t hb = (code_bits(src, rs, re, s_len) + 7) >> 3;
+    const uint32_t hb = (bits + 7) >> 3;
     z.huff = true;
     z.plen = 0;
     if (mode == 0)
         z.size = hb;
     else
     {
-        z.huff = hb < len;                       // strict <, lsqpack.c:848
+        z.huff = hb < len;
         z.plen = z.huff ? hb : len;
         z.size = int_len(z.plen, mode) + z.plen;
     }
     return z;
 }
 
+template <class Src>
+__device__ __forceinline__ EncSize
+size_string(uint32_t mode, const Src &src, uint32_t rs, uint32_t re,
+            const QH_LDS uint8_t *s_len)
+{
+    return size_from_bits(mode, code_bits(src, rs, re, s_len), re - rs);
+}
+
+// ---- byte-parallel dense pass ------------------------------------------------
+
+// OR the right-aligned len-bit value v (len <= 32; v = 0 when len = 0) into
+// the dense stream at bit pos (words hold their bits MSB first, unswapped);
+// positions past the stream are dropped (the tile then falls back)
+__device__ __forceinline__ void
+dense_or(QH_LDS uint32_t *dense, uint32_t pos, uint32_t v, uint32_t len)
+{
+    const uint32_t l = v << ((32u - len) & 31);
+    const uint64_t x = ((uint64_t) l << 32) >> (pos & 31);
+    const uint32_t w = pos >> 5;
+    const uint32_t hi = (uint32_t) (x >> 32), lo = (uint32_t) x;
+    if (w + 1 < (uint32_t) kDenseWords)
+    {
+        __hip_atomic_fetch_or(&dense[w], hi, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lo)
+            __hip_atomic_fetch_or(&dense[w + 1], lo, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// Byte-parallel pass over the tile's staged chunks (lane l holds span chunks
+// l, l + 64, l + 128): code lengths per byte (u8, into the out stage), the
+// dense offset of every chunk (s0) and the codes of all span bytes back to
+// back in `dense` -- the bytes around the tile's strings included (their
+// codes shift every offset by the same amount).  Returns whether the dense
+// stream is usable: every code of the span at most 15 bits.
+__device__ __forceinline__ bool
+dense_pass(const Chunks<kChunks> &ch, uint32_t n16, const QH_LDS uint32_t *mt,
+           QH_LDS EncWave *wv)
+{
+    const uint32_t lane = lane_id();
+    QH_LDS u32x4 *d4 = (QH_LDS u32x4 *) wv->dense;
+    for (uint32_t i = lane; i < (uint32_t) kDenseWords / 4; i += 64)
+        d4[i] = (u32x4){0, 0, 0, 0};
+    wave_sync();
+    QH_LDS u32x4 *lens4 = (QH_LDS u32x4 *) wv->out;
+    uint32_t carry = 0, big = 0;
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k)
+    {
+        if (64u * k >= n16)                    // wave-uniform
+            break;
+        const uint32_t c = lane + 64u * k;
+        const u32x4 w = ch.ch[k];
+        const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            m[j] = mt[(wd[j >> 2] >> (8 * (j & 3))) & 0xffu];
+        uint32_t lp[4], G[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+        {
+            lp[g] = (m[4 * g] >> 27) | ((m[4 * g + 1] >> 27) << 8)
+                  | ((m[4 * g + 2] >> 27) << 16) | ((m[4 * g + 3] >> 27) << 24);
+            G[g] = __builtin_amdgcn_sad_u8(lp[g], 0u, 0u);
+        }
+        big |= (lp[0] | lp[1] | lp[2] | lp[3]) & 0x10101010u;
+        const uint32_t T = G[0] + G[1] + G[2] + G[3];
+        const uint32_t incl = wave_incl_scan(T);
+        const uint32_t p0 = carry + incl - T;
+        carry += read_lane(incl, 63);
+        if (c < n16)
+        {
+            lens4[c] = (u32x4){lp[0], lp[1], lp[2], lp[3]};
+            wv->s0[c] = p0;
+        }
+        uint32_t pos = p0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+        {
+            uint32_t cd[4], L[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+            {
+                cd[j] = m[4 * g + j] & 0x7ffffffu;
+                L[j] = m[4 * g + j] >> 27;
+            }
+            if (__builtin_amdgcn_ballot_w64(G[g] > 32))
+            {
+                // a lane's four codes exceed 32 bits: two pairs of <= 30
+                dense_or(wv->dense, pos, (cd[0] << L[1]) | cd[1], L[0] + L[1]);
+                dense_or(wv->dense, pos + L[0] + L[1], (cd[2] << L[3]) | cd[3],
+                         L[2] + L[3]);
+            }
+            else
+            {
+                uint32_t v = (cd[0] << L[1]) | cd[1];
+                v = (v << L[2]) | cd[2];
+                v = (v << L[3]) | cd[3];
+                dense_or(wv->dense, pos, v, G[g]);
+            }
+            pos += G[g];
+        }
+    }
+    return !__builtin_amdgcn_ballot_w64(big != 0);
+}
+
+// dense offset of span byte p (p <= 16 * n16): the offset of the chunk
+// holding byte p - 1 plus the code lengths of that chunk's bytes before p
+__device__ __forceinline__ uint32_t
+dense_at(const QH_LDS EncWave *wv, uint32_t p)
+{
+    const uint32_t k = (p ? p - 1 : 0) >> 4;
+    const uint32_t nb = p - 16 * k;                      // 0..16 bytes
+    const u32x4 l = ((const QH_LDS u32x4 *) wv->out)[k];
+    const uint32_t ld[4] = {l.x, l.y, l.z, l.w};
+    uint32_t s = wv->s0[k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+        const uint32_t cj = nb > 4u * j ? min(nb - 4u * j, 4u) : 0u;
+        const uint32_t mk = cj >= 4 ? 0xffffffffu : ((1u << (8 * cj)) - 1);
+        s = __builtin_amdgcn_sad_u8(ld[j] & mk, 0u, s);
+    }
+    return s;
+}
+
+// the nb (> 0) dense bits from bit s to the byte-aligned bit d of the output
+// stage (byte order): one 32-bit window of the dense stream per output word;
+// plain stores for the words the string owns whole, OR for its first and
+// last word (shared with framing, padding and the neighbours)
+__device__ __forceinline__ void
+copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
+           QH_LDS uint32_t *st, uint32_t d)
+{
+    const uint32_t e = d + nb;
+    const uint32_t w0 = d >> 5, wl = (e - 1) >> 5, od = d & 31;
+    const uint32_t tailm = 0xffffffffu << (31 - ((e - 1) & 31));
+    {
+        const uint32_t q = s >> 5, os = s & 31;
+        const uint32_t a = dense[q], b = dense[q + 1];
+        uint32_t v = os ? __builtin_amdgcn_alignbit(a, b, 32 - os) : a;
+        v >>= od;
+        if (w0 == wl)
+            v &= tailm;
+        __hip_atomic_fetch_or(&st[w0], bswap32(v), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // output word w0 + k (k >= 1) <- the window at dense bit s - od + 32 k
+    const uint32_t x1 = s - od + 32, sh = x1 & 31;
+    uint32_t q = x1 >> 5;
+    uint32_t cur = dense[q];
+    for (uint32_t w = w0 + 1; w <= wl; ++w)
+    {
+        const uint32_t nxt = dense[q + 1];
+        const uint32_t v = sh ? __builtin_amdgcn_alignbit(cur, nxt, 32 - sh) : cur;
+        if (w == wl)
+            __hip_atomic_fetch_or(&st[w], bswap32(v & tailm), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+            st[w] = bswap32(v);
+        cur = nxt;
+        ++q;
+    }
+}
+
+// one string from the dense stream: framing, payload bits [s, s + bits),
+// padding; raw strings (E3 fallback) from the staged input
+__device__ __forceinline__ void
+emit_dense(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
+           const EncSize &z, const QH_LDS uint32_t *dense, uint32_t s,
+           uint32_t bits, const QH_LDS u32x2 *s_enc, QH_LDS uint32_t *st,
+           uint32_t start)
+{
+    uint32_t pos = 8 * start;
+    if (mode)
+        pos = emit_prefix(st, pos, mode, z.huff, z.plen);
+    if (!z.huff)
+    {
+        pack_bits(in, rs, re, true, s_enc, st, pos);
+        return;
+    }
+    if (bits)
+    {
+        copy_dense(dense, s, bits, st, pos);
+        pos += bits;
+        const uint32_t pad = (8 - (pos & 7)) & 7;
+        if (pad)
+            or_bits(st, pos, (1u << pad) - 1, pad);
+    }
+}
 
 // A tile whose input or output does not fit the stages, coded eagerly:
 // sizes from the stage (given) or from global memory, then packed straight
@@ -480,32 +671,45 @@ struct EncPolicy
     QH_LDS EncSmem *sm;
     QH_LDS EncWave *wv;
     uint32_t rs, re;                 // this lane's string in the stage
+    uint32_t ds, bits;               // its range of the dense stream
     EncSize z;
+    bool dense;                      // wave-uniform: tile from the dense stream
 
+    // staged tile: chunks into the LDS stage, the byte-parallel pass
     __device__ __forceinline__ void stage_in(const Chunks<kChunks> &ch,
-                                             const Span &sp)
+                                             const Span &sp, const TileOffs &)
     {
         ch.store<false>((QH_LDS u32x4 *) wv->in, sp.n16);
+        dense = dense_pass(ch, sp.n16, sm->mt, wv);
     }
     __device__ __forceinline__ const QH_LDS uint32_t *out_stage() const
     {
         return wv->out;
-    }
-    __device__ __forceinline__ QH_LDS uint32_t *hold() const
-    {
-        return wv->hold;
     }
     // staged tile: size this lane's string (E1, and the E3 choice)
     __device__ __forceinline__ void codec(const TileOffs &to, uint32_t cnt,
                                           const Span &sp, uint32_t *sz,
                                           uint32_t *st)
     {
-        const bool valid = lane_id() < cnt;
+        const uint32_t lane = lane_id();
+        const bool valid = lane < cnt;
         rs = valid ? (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa) : 0;
         re = valid ? (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa) : 0;
         z = (EncSize){0, 0, true};
+        if (dense)
+        {
+            // string i spans the dense bits between the offsets of its ends
+            const uint32_t se = dense_at(wv, re);
+            const uint32_t ra = (uint32_t) ((uintptr_t) (in + to.first()) - sp.pa);
+            const uint32_t s_first = dense_at(wv, ra);
+            const uint32_t prev = __shfl_up(se, 1, 64);
+            ds = lane ? prev : s_first;
+            bits = se - ds;
+            dense = read_lane(se, cnt - 1) + 64 <= kDenseBits;
+        }
         if (valid)
-            z = size_string(mode, EncLds{wv->in}, rs, re, sm->len);
+            z = dense ? size_from_bits(mode, bits, re - rs)
+                      : size_string(mode, EncLds{wv->in}, rs, re, sm->len);
         *sz = z.size;
         *st = 0;
     }
@@ -519,8 +723,14 @@ struct EncPolicy
             o4[i] = (u32x4){0, 0, 0, 0};
         wave_sync();
         if (sz)
-            emit_bits(wv->in, rs, re, mode, z.huff, z.plen, sm->enc, wv->out,
-                      excl);
+        {
+            if (dense)
+                emit_dense(wv->in, rs, re, mode, z, wv->dense, ds, bits,
+                           sm->enc, wv->out, excl);
+            else
+                emit_bits(wv->in, rs, re, mode, z.huff, z.plen, sm->enc,
+                          wv->out, excl);
+        }
     }
 
     __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
@@ -534,29 +744,38 @@ struct EncPolicy
     }
 };
 
+// the code tables, loaded once per workgroup (threads 0..256)
+__device__ __forceinline__ void
+enc_tables_load(QH_LDS EncSmem *sm, const uint2 *enc_g, int tid)
+{
+    const QH_GLB u32x2 *genc = (const QH_GLB u32x2 *) enc_g;
+    if (tid < 257)
+    {
+        const u32x2 e = genc[tid];
+        sm->enc[tid] = e;
+        if (tid < 256)
+        {
+            sm->len[tid] = (uint8_t) e.y;
+            sm->mt[tid] = e.y <= 15 ? (e.x | (e.y << 27)) : (31u << 27);
+        }
+    }
+}
+
 __global__ __launch_bounds__(64 * kWaves) void
 qhuff_encode_kernel(EncArgs a)
 {
     __shared__ EncSmem smem;
     QH_LDS EncSmem *sm = (QH_LDS EncSmem *) &smem;
     const int tid = threadIdx.x;
-    {
-        const QH_GLB u32x2 *genc = (const QH_GLB u32x2 *) a.enc;
-        if (tid < 257)
-        {
-            const u32x2 e = genc[tid];
-            sm->enc[tid] = e;
-            if (tid < 256)
-                sm->len[tid] = (uint8_t) e.y;
-        }
-        clear_next_launch(a.c);
-    }
+    enc_tables_load(sm, a.enc, tid);
+    clear_next_launch(a.c);
     __syncthreads();                 // the only workgroup barrier
     EncPolicy pol;
     pol.in = a.in;
     pol.mode = a.mode;
     pol.sm = sm;
     pol.wv = &sm->w[tid >> 6];
+    pol.dense = false;
     tile_pipeline(pol, a.c, a.in, a.in_off, a.n, a.out, a.out_off, nullptr);
 }
 

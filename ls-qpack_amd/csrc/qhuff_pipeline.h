@@ -3,28 +3,32 @@
 //
 // Wave g codes tiles g, g + W, g + 2W, ... (W = waves in the grid; the grid
 // is at most what is co-resident, so every tile a look-back waits on belongs
-// to a running wave).  Per iteration, for tile t (input already in the LDS
-// stage):
+// to a running wave).  Per iteration, for tile t:
 //
-//   top    one wait for everything the last iteration issued (issued about
-//          a codec ago, so it has landed); the previous tile's super-
-//          accumulator add has returned: if it completed its super tile,
-//          publish the super aggregate; write t's input (loaded last
-//          iteration) into the stage; load the next tile's input and the
-//          offsets of the one after it; poll the previous tile's look-back
-//          windows
+//   top    one wait for everything the last iteration issued, a whole codec
+//          ago: t's input chunks and offsets, the older pending tile's
+//          look-back polls, the newer one's super-accumulator add, the
+//          stores of the tile before.  Publish the newer tile's super
+//          aggregate if its add completed the super tile; resolve the older
+//          pending tile's look-back and store its output (registers).
+//          P::stage_in() -- t's chunks into the LDS stage (the encoder also
+//          runs its byte-parallel pass here, on the chunk registers) -- then
+//          issue the loads of the next tile's input and of the offsets of
+//          the tile after it, so they have the whole codec to land
 //   codec  P::codec() -- LDS only -- per-lane output size (+ status)
 //   scan   wave scan -> tile-local offsets, tile total; publish the tile
 //          aggregate and add it to the super accumulator (LookBack::start)
-//   defer  resolve the look-back of the tile coded TWO iterations ago (its
-//          polls were issued at the top, a codec ago) and store its output
-//          (parked in the wave's LDS hold buffer), offsets and status; park
-//          the previous tile's output (registers) in the hold buffer
 //   emit   P::emit() -- compacted output of t into the LDS out stage --
-//          gathered into registers (TileOut), to be stored next iteration
+//          gathered into registers (TileOut)
+//   poll   issue the older pending tile's look-back polls
+//
+// Two tiles are pending at a time, both holding their output in registers:
+// tile k's look-back is resolved at the top of iteration k + 2, its windows
+// polled at the end of iteration k + 1, a whole codec after every tile
+// before it published its aggregate.
 //
 // Tiles whose input or output does not fit the stages are coded eagerly by
-// P::slow_tile() (out of line) after the deferred tile has been flushed.
+// P::slow_tile() (out of line) after the pending tile has been flushed.
 #pragma once
 
 #include "qhuff_kernels.h"
@@ -35,8 +39,7 @@ constexpr int kChunks = 3;                  // 16-byte input chunks per lane
 constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: input / output stage
 
 // A coded tile waiting for its look-back: per-lane output offset and status,
-// the look-back state.  Its output bytes wait in registers (the newer of the
-// two deferred tiles) or in the wave's LDS hold buffer (the older).
+// the look-back state; its output bytes wait in registers (TileOut).
 struct Pending
 {
     bool valid;
@@ -67,18 +70,6 @@ flush_tile(const Coord &c, Pending &d, const TileOut<kChunks> &o, uint8_t *out,
     if (d.tile == c.n_tiles - 1 && lane == 0)
         ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + d.total);
     d.valid = false;
-}
-
-// the older pending tile, output from the hold buffer
-template <bool kStatus>
-__device__ __forceinline__ void
-flush_held(const Coord &c, Pending &d, QH_LDS uint32_t *hold,
-           uint8_t *out, uint32_t *out_off, uint8_t *status, uint64_t n,
-           uint32_t it = ~0u)
-{
-    TileOut<kChunks> o;
-    o.gather(hold);
-    flush_tile<kStatus>(c, d, o, out, out_off, status, n, it);
 }
 
 // vmcnt(0), other counters untouched (gfx9 s_waitcnt encoding)
@@ -128,8 +119,7 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
     // large register set is live across a codec.
     Pending older, newer;
     older.valid = newer.valid = false;
-    TileOut<kChunks> newer_out;
-    QH_LDS uint32_t *hold = pol.hold();
+    TileOut<kChunks> older_out, newer_out;
     uint32_t it = 0;
     for (uint64_t tile_k = t;; ++it)
     {
@@ -142,16 +132,19 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
         if (newer.valid)
             newer.lb.super_agg(c);
         if (older.valid)
-            flush_held<P::kStatus>(c, older, hold, out, out_off, status, n,
-                                   it);
-        wave_sync();
-        if (newer.valid)
-            newer_out.park(hold);
+            flush_tile<P::kStatus>(c, older, older_out, out, out_off, status,
+                                   n, it);
         older = newer;
+        older_out = newer_out;
         newer.valid = false;
         if (sp_cur.staged)
-            pol.stage_in(ch, sp_cur);
+            pol.stage_in(ch, sp_cur, o_cur);
         wave_sync();
+        // loads for the next tile, a whole codec ahead of their use
+        const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), kStageCap);
+        ch.load(sp_nxt);
+        const uint32_t tz = clamp(tile_k + 2ull * W);
+        o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
         prof_stamp(c, it, 2);
 
         // codec of t (LDS only when staged)
@@ -165,12 +158,6 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
         const uint32_t total = read_lane(incl, 63);
         fast = fast && total + 64 <= (uint32_t) kStageCap;
         prof_stamp(c, it, 3);
-
-        // loads for the next tile
-        const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), kStageCap);
-        ch.load(sp_nxt);
-        const uint32_t tz = clamp(tile_k + 2ull * W);
-        o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
 
         if (fast)
         {
@@ -193,7 +180,7 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
             if (older.valid)
             {
                 older.lb.poll(c);
-                flush_held<P::kStatus>(c, older, hold, out, out_off, status, n);
+                flush_tile<P::kStatus>(c, older, older_out, out, out_off, status, n);
             }
             pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
                           status, n);
@@ -216,7 +203,7 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
     if (newer.valid)
         newer.lb.super_agg(c);
     if (older.valid)
-        flush_held<P::kStatus>(c, older, hold, out, out_off, status, n);
+        flush_tile<P::kStatus>(c, older, older_out, out, out_off, status, n);
     if (newer.valid)
     {
         newer.lb.poll(c);

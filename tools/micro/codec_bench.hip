@@ -25,14 +25,7 @@ mb_encode(EncArgs a, int reps, MbOut *res)
     __shared__ EncSmem smem;
     QH_LDS EncSmem *sm = (QH_LDS EncSmem *) &smem;
     const int tid = threadIdx.x;
-    const QH_GLB u32x2 *genc = (const QH_GLB u32x2 *) a.enc;
-    if (tid < 257)
-    {
-        const u32x2 e = genc[tid];
-        sm->enc[tid] = e;
-        if (tid < 256)
-            sm->len[tid] = (uint8_t) e.y;
-    }
+    enc_tables_load(sm, a.enc, tid);
     __syncthreads();
     QH_LDS EncWave *wv = &sm->w[tid >> 6];
     const uint32_t gid = blockIdx.x * W + (tid >> 6), lane = lane_id();
@@ -42,8 +35,6 @@ mb_encode(EncArgs a, int reps, MbOut *res)
     const Span sp = tile_span(a.in, to.first(), to.last(), kStageCap);
     Chunks<kChunks> ch;
     ch.load(sp);
-    ch.store<false>((QH_LDS u32x4 *) wv->in, sp.n16);
-    wave_sync();
     EncPolicy pol;
     pol.in = a.in;
     pol.mode = a.mode;
@@ -53,6 +44,8 @@ mb_encode(EncArgs a, int reps, MbOut *res)
     for (int r = 0; r < reps; ++r)
     {
         const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        pol.stage_in(ch, sp, to);            // dense pass included
+        wave_sync();
         uint32_t sz, st;
         pol.codec(to, kWT, sp, &sz, &st);
         const uint32_t incl = wave_incl_scan(sz);
