@@ -267,21 +267,26 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
     // one loop, no lane branches: a lane with < 32 real bits left steps with
     // c = ns = 0 (its two arena byte writes land at its current end and are
     // overwritten by the epilogue); the long-code fix is computed for the
-    // whole wave with selects, behind a wave-uniform branch
+    // whole wave with selects, behind a wave-uniform branch.  The next
+    // window is taken from the shifted buffer BEFORE the refill: a step of
+    // <= 12 bits leaves >= 20 valid bits, so the step's dependency chain is
+    // lookup -> length -> shift -> index, with the refill beside it (after a
+    // long code the index is recomputed behind a second uniform branch)
+    uint32_t idx = (uint32_t) (buf >> (64 - kWinBits));
     if (__builtin_amdgcn_ballot_w64(rem >= 32))
     do
     {
         const bool act = rem >= 32;
-        const uint32_t hi = (uint32_t) (buf >> 32);
-        uint32_t e = s_win[hi >> (32 - kWinBits)];
+        uint32_t e = s_win[idx];
         uint32_t c = (e >> 16) & 15;          // bits of the entry's symbols
         uint32_t ns = (e >> 24) & 3;          // symbols (0: longer code)
-        if (__builtin_amdgcn_ballot_w64(act & (e < (1u << 24))))
+        const bool lng = act & (e < (1u << 24));
+        const bool any_long = __builtin_amdgcn_ballot_w64(lng) != 0;
+        if (any_long)
         {
             // a code of 13..30 bits (EOS rejects the string, D3 (a))
-            const bool lng = act & (e < (1u << 24));
             uint32_t L;
-            const uint32_t sym = long_code(hi, s_sorted, &L);
+            const uint32_t sym = long_code((uint32_t) (buf >> 32), s_sorted, &L);
             const bool eos = lng & (sym == 256);
             e = lng ? sym : e;
             c = lng ? (eos ? 0u : L) : c;
@@ -291,8 +296,9 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         }
         c = act ? c : 0u;
         ns = act ? ns : 0u;
-        emit(e, ns);
         buf <<= c;
+        idx = (uint32_t) (buf >> (64 - kWinBits));
+        emit(e, ns);
         bits -= c;
         rem -= c;
         const bool need = bits < 32;
@@ -300,8 +306,9 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         buf |= (uint64_t) dd << ((32 - bits) & 31);
         bits += need ? 32u : 0u;
         p += need ? 1u : 0u;
-        if (need)
-            nx = src[p];
+        nx = src[p];
+        if (any_long)
+            idx = (uint32_t) (buf >> (64 - kWinBits));
     } while (__builtin_amdgcn_ballot_w64(rem >= 32));
 
     // epilogue: the last < 32 bits, padded with ones; D3 tail rule
@@ -341,6 +348,7 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         rem -= c;
         fin = fin | over | eos | (rem == 0);
     } while (__builtin_amdgcn_ballot_w64(!fin));
+    emit.finish();
     return bad ? -1 : (int) emit.n;
 }
 
@@ -350,6 +358,7 @@ struct ArenaEmit
 {
     QH_LDS uint8_t *slot;
     uint32_t n;
+    __device__ __forceinline__ void finish() {}
     __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
     {
 #if QH_EMIT_B16
@@ -360,6 +369,40 @@ struct ArenaEmit
         slot[n + 1] = (uint8_t) (val >> 8);
 #endif
         n += nb;
+    }
+};
+
+// arena sink accumulating bytes in registers: whole dwords go to a
+// dword-aligned arena slot as they fill (one LDS store per four output bytes
+// instead of two per step).  Measured slower than ArenaEmit on MI355X -- the
+// decode loop is issue/latency-bound, not LDS-bound -- kept for experiments;
+// finish() stores the partial last dword and sets n
+struct WordEmit
+{
+    QH_LDS uint32_t *slot;
+    uint32_t w;                      // dwords stored
+    uint32_t sh;                     // bits pending in acc: 0, 8, 16 or 24
+    uint64_t acc;
+    uint32_t n;                      // output bytes (after finish())
+    __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
+    {
+        // the entry's first nb symbol bytes (nb <= 2)
+        const uint32_t v = val & ((1u << (8 * nb)) - 1);
+        acc |= (uint64_t) v << sh;
+        sh += 8 * nb;
+        if (sh >= 32)
+        {
+            slot[w] = (uint32_t) acc;
+            acc >>= 32;
+            sh -= 32;
+            ++w;
+        }
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if (sh)
+            slot[w] = (uint32_t) acc;
+        n = 4 * w + sh / 8;
     }
 };
 

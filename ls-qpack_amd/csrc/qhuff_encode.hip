@@ -470,8 +470,9 @@ dense_pass(const Chunks<kChunks> &ch, uint32_t n16, const QH_LDS uint32_t *mt,
 #pragma unroll
     for (int k = 0; k < kChunks; ++k)
     {
-        if (64u * k >= n16)                    // wave-uniform
-            break;
+        // every row is coded (no exit for short spans): straight-line code
+        // lets the rows' lookups overlap; chunks past the span are clamped
+        // copies of its last chunk, coded past its end and never read
         const uint32_t c = lane + 64u * k;
         const u32x4 w = ch.ch[k];
         const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
@@ -573,6 +574,7 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
     const uint32_t x1 = s - od + 32, sh = x1 & 31;
     uint32_t q = x1 >> 5;
     uint32_t cur = dense[q];
+#pragma unroll 2
     for (uint32_t w = w0 + 1; w <= wl; ++w)
     {
         const uint32_t nxt = dense[q + 1];

@@ -35,6 +35,12 @@
 
 namespace qhuff {
 
+// 1: the next tile's input / offsets are loaded right after the current
+// tile is staged (a whole codec ahead); 0: after the codec
+#ifndef QH_EARLY_LOADS
+#define QH_EARLY_LOADS 1
+#endif
+
 constexpr int kChunks = 3;                  // 16-byte input chunks per lane
 constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: input / output stage
 
@@ -142,9 +148,11 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
         wave_sync();
         // loads for the next tile, a whole codec ahead of their use
         const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), kStageCap);
+#if QH_EARLY_LOADS
         ch.load(sp_nxt);
         const uint32_t tz = clamp(tile_k + 2ull * W);
         o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
+#endif
         prof_stamp(c, it, 2);
 
         // codec of t (LDS only when staged)
@@ -158,6 +166,11 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
         const uint32_t total = read_lane(incl, 63);
         fast = fast && total + 64 <= (uint32_t) kStageCap;
         prof_stamp(c, it, 3);
+#if !QH_EARLY_LOADS
+        ch.load(sp_nxt);
+        const uint32_t tz = clamp(tile_k + 2ull * W);
+        o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
+#endif
 
         if (fast)
         {
