@@ -151,6 +151,30 @@ struct qhuff_decode_retval
 qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, int src_len,
                   unsigned char *dst, int dst_len);
 
+/* ---- header hashing ---------------------
+ * XXH32 (deps/xxhash/xxhash.c) of header names and values, as the reference
+ * computes it for every header it encodes (lsqpack.c:1681-1685) or decodes
+ * (lsqpack.c:3268-3269, 3308-3309), seeded with LSQPACK_XXH_SEED
+ * (lsqpack.c:623) to index its static and dynamic tables. */
+#define QHUFF_XXH_SEED 39378473u
+
+/* n headers (device pointers); header i is name in[off[2i] .. off[2i+1])
+ * followed by value in[off[2i+1] .. off[2i+2]) (2n + 1 offsets, the name /
+ * value layout of an lsxpack_header buffer).  Writes
+ *   name_hash[i]    = XXH32(name,  name_len,  seed)
+ *   nameval_hash[i] = XXH32(value, value_len, name_hash[i]).
+ * Asynchronous on `stream`. */
+int qhuff_xxh32_headers(qhuff_ctx *ctx, const uint8_t *in,
+                        const uint32_t *off, uint32_t n, uint32_t seed,
+                        uint32_t *name_hash, uint32_t *nameval_hash,
+                        void *stream);
+
+/* n independent strings (device pointers, n + 1 offsets as in the codec
+ * batches): hash[i] = XXH32(string i, seed).  Asynchronous on `stream`. */
+int qhuff_xxh32_batch(qhuff_ctx *ctx, const uint8_t *in,
+                      const uint32_t *in_off, uint32_t n, uint32_t seed,
+                      uint32_t *hash, void *stream);
+
 /* Last HIP error string for this context (diagnostics). */
 const char *qhuff_last_error(qhuff_ctx *ctx);
 

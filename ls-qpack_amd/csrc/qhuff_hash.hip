@@ -1,0 +1,216 @@
+// qhuff_hash.hip -- batched XXH32 of header names and values (gfx950).
+//
+// Reference: every header the encoder takes
+// and every header the decoder emits is hashed twice with XXH32
+// (deps/xxhash/xxhash.c, 32-bit variant):
+//
+//   name_hash    = XXH32(name,  name_len,  LSQPACK_XXH_SEED)  lsqpack.c:1681,
+//                                                             3268-3269
+//   nameval_hash = XXH32(value, value_len, name_hash)         lsqpack.c:1685,
+//                                                             3308-3309
+//
+// (LSQPACK_XXH_SEED = 39378473, lsqpack.c:623).  The hashes index the static
+// table (name2id_plus_one / nameval2id_plus_one, lsqpack.c:629-753) and the
+// dynamic table.  Like the Huffman kernels this is per-string byte work:
+// one header per lane, one 64-header tile per wave, the tile's contiguous
+// name/value bytes staged into the wave's LDS region with coalesced 16-byte
+// loads, then each lane walks its own bytes out of LDS (four 32-bit
+// accumulators over 16-byte stripes, then 4-byte and 1-byte tails).  The
+// outputs are fixed-size (two u32 per header), so no scan or look-back is
+// needed and the grid is simply one wave per tile.  HBM-bound: a header
+// costs its name + value bytes + 8 B of offsets + 8 B of hashes.
+#include "qhuff_kernels.h"
+
+namespace qhuff {
+
+constexpr int kHashWaves = 8;                      // waves per workgroup
+constexpr int kHashNch = 6;                        // 16-byte chunks per lane
+constexpr uint32_t kHashCap = 64 * kHashNch * 16;  // staged bytes per wave
+
+constexpr uint32_t kP1 = 2654435761u, kP2 = 2246822519u, kP3 = 3266489917u,
+                   kP4 = 668265263u, kP5 = 374761393u;
+
+__device__ __forceinline__ uint32_t
+rotl32(uint32_t x, uint32_t r)
+{
+    return __builtin_amdgcn_alignbit(x, x, 32 - r);
+}
+
+__device__ __forceinline__ uint32_t
+xxh_round(uint32_t acc, uint32_t w)
+{
+    return rotl32(acc + w * kP2, 13) * kP1;
+}
+
+// bytes staged in LDS; byte index i = global address - 16-aligned span base
+struct HashLds
+{
+    const QH_LDS uint32_t *s;
+    __device__ __forceinline__ uint32_t word(uint32_t i) const
+    {
+        const uint32_t q = i >> 2;
+        return align_bytes(s[q + 1], s[q], i & 3);
+    }
+    __device__ __forceinline__ void stripe(uint32_t i, uint32_t w[4]) const
+    {
+        const uint32_t q = i >> 2, sh = i & 3;
+        const uint32_t d0 = s[q], d1 = s[q + 1], d2 = s[q + 2], d3 = s[q + 3],
+                       d4 = s[q + 4];
+        w[0] = align_bytes(d1, d0, sh);
+        w[1] = align_bytes(d2, d1, sh);
+        w[2] = align_bytes(d3, d2, sh);
+        w[3] = align_bytes(d4, d3, sh);
+    }
+    __device__ __forceinline__ uint32_t byte(uint32_t i) const
+    {
+        return ((const QH_LDS uint8_t *) s)[i];
+    }
+};
+
+// bytes read straight from global (tiles too large for the stage): byte
+// loads only, so nothing outside the string is touched
+struct HashGlb
+{
+    const QH_GLB uint8_t *p;
+    __device__ __forceinline__ uint32_t byte(uint32_t i) const { return p[i]; }
+    __device__ __forceinline__ uint32_t word(uint32_t i) const
+    {
+        return p[i] | (p[i + 1] << 8) | (p[i + 2] << 16)
+             | ((uint32_t) p[i + 3] << 24);
+    }
+    __device__ __forceinline__ void stripe(uint32_t i, uint32_t w[4]) const
+    {
+        w[0] = word(i);
+        w[1] = word(i + 4);
+        w[2] = word(i + 8);
+        w[3] = word(i + 12);
+    }
+};
+
+// XXH32 of bytes [a, a + len) (xxhash.c XXH32 / XXH32_endian_align):
+// 16-byte stripes into four lanes, merge, + len, 4-byte then 1-byte tail,
+// avalanche
+template <class R>
+__device__ __forceinline__ uint32_t
+xxh32(const R &r, uint32_t a, uint32_t len, uint32_t seed)
+{
+    uint32_t p = a;
+    const uint32_t end = a + len;
+    uint32_t h;
+    if (len >= 16)
+    {
+        uint32_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed,
+                 v4 = seed - kP1;
+        const uint32_t limit = end - 16;
+        do
+        {
+            uint32_t w[4];
+            r.stripe(p, w);
+            v1 = xxh_round(v1, w[0]);
+            v2 = xxh_round(v2, w[1]);
+            v3 = xxh_round(v3, w[2]);
+            v4 = xxh_round(v4, w[3]);
+            p += 16;
+        } while (p <= limit);
+        h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
+    }
+    else
+        h = seed + kP5;
+    h += len;
+    while (p + 4 <= end)
+    {
+        h += r.word(p) * kP3;
+        h = rotl32(h, 17) * kP4;
+        p += 4;
+    }
+    while (p < end)
+    {
+        h += r.byte(p) * kP5;
+        h = rotl32(h, 11) * kP1;
+        ++p;
+    }
+    h ^= h >> 15;
+    h *= kP2;
+    h ^= h >> 13;
+    h *= kP3;
+    h ^= h >> 16;
+    return h;
+}
+
+struct HashWave
+{
+    alignas(16) uint32_t s[kHashCap / 4 + 8];      // + slack for stripe reads
+};
+
+template <class R>
+__device__ __forceinline__ void
+hash_lane(const R &r, bool pairs, uint32_t a, uint32_t m, uint32_t b,
+          uint32_t seed, uint32_t *h1, uint32_t *h2)
+{
+    if (pairs)
+    {
+        *h1 = xxh32(r, a, m - a, seed);
+        *h2 = xxh32(r, m, b - m, *h1);
+    }
+    else
+        *h1 = xxh32(r, a, b - a, seed);
+}
+
+__global__ __launch_bounds__(64 * kHashWaves) void
+qhuff_hash_kernel(HashArgs a)
+{
+    __shared__ HashWave sm[kHashWaves];
+    const uint32_t lane = lane_id();
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint64_t t = (uint64_t) blockIdx.x * kHashWaves + wv;
+    const uint64_t s0 = t * kWT;
+    if (s0 >= a.n)
+        return;
+    const uint32_t cnt = (uint32_t) min((uint64_t) kWT, a.n - s0);
+    const uint32_t k = a.pairs ? 2 : 1;             // offsets per header
+    const QH_GLB uint32_t *off = glb(a.off) + s0 * k;
+    const uint32_t li = lane < cnt ? lane : cnt - 1;
+    const uint32_t oa = off[k * li];
+    const uint32_t om = off[k * li + 1];
+    const uint32_t ob = a.pairs ? off[k * li + 2] : om;
+    const uint32_t first = read_lane(oa, 0);
+    const uint32_t last = read_lane(ob, cnt - 1);
+    const Span sp = tile_span(a.in, first, last, kHashCap);
+    uint32_t h1 = 0, h2 = 0;
+    if (sp.staged)
+    {
+        Chunks<kHashNch> ch;
+        ch.load(sp);
+        QH_LDS uint32_t *s = (QH_LDS uint32_t *) sm[wv].s;
+        ch.store<false>((QH_LDS u32x4 *) s, sp.n16);
+        wave_sync();
+        // byte index of input offset x in the stage: x - first + skew
+        const uint32_t skew = (uint32_t) ((uintptr_t) (a.in + first) - sp.pa);
+        const HashLds r{s};
+        hash_lane(r, a.pairs, oa - first + skew, om - first + skew,
+                  ob - first + skew, a.seed, &h1, &h2);
+    }
+    else
+    {
+        const HashGlb r{glb(a.in)};
+        hash_lane(r, a.pairs, oa, om, ob, a.seed, &h1, &h2);
+    }
+    if (lane < cnt)
+    {
+        glb(a.h1)[s0 + lane] = h1;
+        if (a.pairs)
+            glb(a.h2)[s0 + lane] = h2;
+    }
+}
+
+hipError_t
+launch_hash(const HashArgs &a, hipStream_t st)
+{
+    const uint64_t tiles = (a.n + kWT - 1) / kWT;
+    const uint32_t grid = (uint32_t) ((tiles + kHashWaves - 1) / kHashWaves);
+    hipLaunchKernelGGL(qhuff_hash_kernel, dim3(grid), dim3(64 * kHashWaves),
+                       0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace qhuff

@@ -367,6 +367,47 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     return QHUFF_OK;
 }
 
+// ---- header hashing ---------------------------------------------------------
+
+static int
+hash_call(qhuff_ctx *c, const uint8_t *in, const uint32_t *off, uint32_t n,
+          uint32_t seed, uint32_t *h1, uint32_t *h2, bool pairs, void *stream)
+{
+    if (!c || !off || (n && (!in || !h1 || (pairs && !h2))))
+        return QHUFF_EINVAL;
+    if (pairs && n > 0x7fffffffu)
+        return QHUFF_ERANGE;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n == 0)
+        return QHUFF_OK;
+    HashArgs a;
+    a.in = in;
+    a.off = off;
+    a.h1 = h1;
+    a.h2 = h2;
+    a.n = n;
+    a.seed = seed;
+    a.pairs = pairs ? 1u : 0u;
+    HIPCHK(c, launch_hash(a, (hipStream_t) stream));
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_xxh32_headers(qhuff_ctx *c, const uint8_t *in, const uint32_t *off,
+                    uint32_t n, uint32_t seed, uint32_t *name_hash,
+                    uint32_t *nameval_hash, void *stream)
+{
+    return hash_call(c, in, off, n, seed, name_hash, nameval_hash, true,
+                     stream);
+}
+
+extern "C" int
+qhuff_xxh32_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
+                  uint32_t n, uint32_t seed, uint32_t *hash, void *stream)
+{
+    return hash_call(c, in, in_off, n, seed, hash, nullptr, false, stream);
+}
+
 // ---- host-memory path ------------------------------------------------------
 
 static int

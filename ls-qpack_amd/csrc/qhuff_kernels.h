@@ -43,6 +43,17 @@ struct DecArgs
     LongParams lp;
 };
 
+struct HashArgs
+{
+    const uint8_t *in;
+    const uint32_t *off;         // pairs: 2n + 1 offsets, else n + 1
+    uint32_t *h1;                // name hash (pairs) / string hash
+    uint32_t *h2;                // name+value hash (pairs only)
+    uint64_t n;
+    uint32_t seed;
+    uint32_t pairs;
+};
+
 template <class T>
 __device__ __forceinline__ const QH_GLB T *
 glb(const T *p)
@@ -59,6 +70,7 @@ glb(T *p)
 
 hipError_t launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st);
 hipError_t launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st);
+hipError_t launch_hash(const HashArgs &a, hipStream_t st);
 hipError_t encode_occupancy(int *blocks_per_cu);
 hipError_t decode_occupancy(int *blocks_per_cu);
 size_t encode_lds_bytes();

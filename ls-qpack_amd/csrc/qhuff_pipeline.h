@@ -91,7 +91,6 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
               uint64_t n, uint8_t *out, uint32_t *out_off, uint8_t *status)
 {
     const QH_GLB uint32_t *in_off = (const QH_GLB uint32_t *) in_off_p;
-    const uint32_t lane = lane_id();
     const uint32_t W = gridDim.x * kWaves;
     const uint32_t nt = c.n_tiles;
     uint32_t t = blockIdx.x * kWaves + (threadIdx.x >> 6);

@@ -26,7 +26,10 @@ EXPORTS = (
     "qhuff_decode_batch_host", "qhuff_enc_enc_str", "qhuff_enc_str_size",
     "qhuff_huff_decode", "qhuff_last_error", "qhuff_shard_cuts",
     "qhuff_synth_batch", "qhuff_device_error", "qhuff_profile_read",
+    "qhuff_xxh32_headers", "qhuff_xxh32_batch",
 )
+
+XXH_SEED = 39378473                       # LSQPACK_XXH_SEED, lsqpack.c:623
 
 
 class QhuffError(RuntimeError):
@@ -87,6 +90,12 @@ def lib():
         L.qhuff_synth_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32,
                                         C.c_uint32, C.c_char_p, C.c_uint32,
                                         vp, u32p]
+        L.qhuff_xxh32_headers.restype = C.c_int
+        L.qhuff_xxh32_headers.argtypes = [vp, vp, u32p, C.c_uint32,
+                                          C.c_uint32, u32p, u32p, vp]
+        L.qhuff_xxh32_batch.restype = C.c_int
+        L.qhuff_xxh32_batch.argtypes = [vp, vp, u32p, C.c_uint32, C.c_uint32,
+                                        u32p, vp]
         _lib = L
     return _lib
 
@@ -223,6 +232,38 @@ class Codec:
         status = torch.empty(max(n, 1), dtype=torch.uint8, device=data.device)
         self.decode_into(data, in_off, n, out, out_off, status, stream)
         return out, out_off, status[:n]
+
+    # header hashing (XXH32, lsqpack.c:1681-1685) ---------------------------
+    def xxh32_headers_into(self, data, off, n, seed, name_hash, nameval_hash,
+                           stream=None):
+        rc = lib().qhuff_xxh32_headers(self._ctx, data.data_ptr(),
+                                       off.data_ptr(), n, seed,
+                                       name_hash.data_ptr(),
+                                       nameval_hash.data_ptr(),
+                                       self._stream(stream))
+        self._check(rc, "qhuff_xxh32_headers")
+
+    def xxh32_headers(self, data, off, seed=XXH_SEED, stream=None):
+        """off: int32 cuda tensor [2n+1] (name, value, name, value ...).
+        Returns (name_hash, nameval_hash) int32 tensors [n] (uint32 bits)."""
+        import torch
+        n = (off.numel() - 1) // 2
+        h1 = torch.empty(max(n, 1), dtype=torch.int32, device=data.device)
+        h2 = torch.empty(max(n, 1), dtype=torch.int32, device=data.device)
+        self.xxh32_headers_into(data, off, n, seed & 0xffffffff, h1, h2,
+                                stream)
+        return h1[:n], h2[:n]
+
+    def xxh32(self, data, in_off, seed=XXH_SEED, stream=None):
+        """hash[i] = XXH32(string i, seed); int32 tensor [n]."""
+        import torch
+        n = in_off.numel() - 1
+        h = torch.empty(max(n, 1), dtype=torch.int32, device=data.device)
+        rc = lib().qhuff_xxh32_batch(self._ctx, data.data_ptr(),
+                                     in_off.data_ptr(), n, seed & 0xffffffff,
+                                     h.data_ptr(), self._stream(stream))
+        self._check(rc, "qhuff_xxh32_batch")
+        return h[:n]
 
     # host-memory batch calls (numpy) ----------------------------------------
     def encode_host(self, data, in_off, mode=ENC_PAYLOAD):

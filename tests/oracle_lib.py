@@ -25,9 +25,10 @@ class DecState(C.Structure):
 
 
 def build():
-    src = os.path.join(ORACLE_DIR, "qhuff_oracle.c")
-    if (not os.path.exists(ORACLE_SO)
-            or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src)):
+    srcs = [os.path.join(ORACLE_DIR, f)
+            for f in ("qhuff_oracle.c", "xxh32_oracle.c")]
+    if (not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO)
+            < max(os.path.getmtime(s) for s in srcs)):
         subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
     return ORACLE_SO
 
@@ -68,8 +69,32 @@ def lib():
         L.oq_code_of.restype = None
         L.oq_code_of.argtypes = [C.c_uint, C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_uint)]
+        L.oq_xxh32.restype = C.c_uint32
+        L.oq_xxh32.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
+        L.oq_xxh32_headers.restype = None
+        L.oq_xxh32_headers.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32,
+                                       C.c_uint32, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
+
+
+XXH_SEED = 39378473                       # LSQPACK_XXH_SEED, lsqpack.c:623
+
+
+def xxh32(s: bytes, seed: int = XXH_SEED) -> int:
+    return lib().oq_xxh32(s, len(s), seed & 0xffffffff)
+
+
+def xxh32_headers(data: np.ndarray, off: np.ndarray, seed: int = XXH_SEED):
+    """off[2n+1] (name, value, ...) -> (name_hash, nameval_hash) uint32[n]."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint32)
+    n = (len(off) - 1) // 2
+    h1 = np.zeros(max(n, 1), dtype=np.uint32)
+    h2 = np.zeros(max(n, 1), dtype=np.uint32)
+    lib().oq_xxh32_headers(_p(data), _p(off), n, seed & 0xffffffff, _p(h1),
+                           _p(h2))
+    return h1[:n], h2[:n]
 
 
 # ---- per-string helpers --------------------------------------------------
