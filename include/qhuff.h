@@ -151,6 +151,76 @@ struct qhuff_decode_retval
 qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, int src_len,
                   unsigned char *dst, int dst_len);
 
+/* ---- literal-span pre-parse + batched literal decode (SURVEY.md 8(f)
+ * rank 3).  A host pass walks only the instruction framing of QPACK wire
+ * data -- field sections (RFC 9204 4.5; the reference's parse_header_prefix /
+ * parse_header_data, lsqpack.c:3955-4046, 3567-3915) and encoder-stream
+ * instructions (RFC 9204 4.3; lsqpack_dec_enc_in, lsqpack.c:4574-4960) --
+ * with the reference's integer rules (lsqpack_dec_int / _int24,
+ * lsqpack.c:2372-2460), and records every string literal.  Indices are not
+ * resolved: the dynamic table stays with the reference.  The literals of
+ * any number of blocks are then decoded in one GPU launch. */
+#define QHUFF_EPROTO    (-71)   /* malformed instruction (bad integer)     */
+#define QHUFF_ETRUNC    (-61)   /* input ends inside an instruction        */
+
+#define QHUFF_LIT_NAME   1
+#define QHUFF_LIT_VALUE  2
+
+struct qhuff_literal
+{
+    uint32_t pos;               /* payload offset: pos_base + offset in buf */
+    uint32_t len;               /* payload bytes                            */
+    uint8_t  huffman;           /* H bit                                    */
+    uint8_t  prefix_bits;       /* 3, 5 or 7: its length prefix             */
+    uint8_t  kind;              /* QHUFF_LIT_NAME / QHUFF_LIT_VALUE         */
+    uint8_t  reserved;
+    uint32_t instr;             /* pos_base + offset of its instruction     */
+};
+
+/* One complete encoded field section (prefix + field lines).  Writes up to
+ * max_lits literals in wire order and the count to *n_lits.  QHUFF_OK,
+ * QHUFF_ETRUNC (ends inside a line), QHUFF_EPROTO (an integer the reference
+ * rejects), QHUFF_ERANGE (*n_lits is the count needed). */
+int qhuff_scan_field_section(const uint8_t *buf, size_t len, uint32_t pos_base,
+                             struct qhuff_literal *lits, uint32_t max_lits,
+                             uint32_t *n_lits);
+
+/* Encoder-stream bytes (may end inside an instruction: *consumed is the
+ * length of the complete instructions, whose literals are reported; the
+ * caller keeps the rest for the next chunk, as the reference resumes). */
+int qhuff_scan_encoder_stream(const uint8_t *buf, size_t len,
+                              uint32_t pos_base, struct qhuff_literal *lits,
+                              uint32_t max_lits, uint32_t *n_lits,
+                              size_t *consumed);
+
+/* Output bytes qhuff_decode_literals_host may write for these literals. */
+uint64_t qhuff_literals_bound(const struct qhuff_literal *lits, uint32_t n);
+
+/* Decode n literals whose payloads lie in host buffer `buf` (lits[i].pos is
+ * relative to buf): Huffman ones (H = 1) on the GPU in one batch, with the
+ * lsqpack_huff_decode semantics of qhuff_decode_batch; raw ones copied.
+ * Host out_off[n + 1], status[n] (QHUFF_DEC_OK / QHUFF_DEC_ERROR, an ERROR
+ * literal contributes 0 bytes).  `out` holds qhuff_literals_bound bytes.
+ * Synchronous. */
+int qhuff_decode_literals_host(qhuff_ctx *ctx, const uint8_t *buf,
+                               const struct qhuff_literal *lits, uint32_t n,
+                               uint8_t *out, uint32_t *out_off,
+                               uint8_t *status);
+
+/* ---- encoder-side hook ---------------------------
+ * lsqpack_enc_enc_str (lsqpack.c:839-876) for a string whose Huffman
+ * payload was precomputed by a QHUFF_ENC_PAYLOAD batch (huff, huff_len =
+ * that batch's output i; huff_len is also qenc_enc_str_size, the figure the
+ * ratio guard at lsqpack.c:1946-1957 reads).  Same bytes, return value and
+ * -1 on short dst_len as the reference; bits of dst[0] above the H bit are
+ * kept.  Host-only, no device call: a patched lsqpack.c calls it per literal
+ * after batch-encoding every name and value of a header list up front
+ * (INTEGRATION.md). */
+int qhuff_frame_literal(unsigned prefix_bits, unsigned char *dst,
+                        size_t dst_len, const unsigned char *str,
+                        unsigned str_len, const unsigned char *huff,
+                        unsigned huff_len);
+
 /* ---- header hashing ---------------------
  * XXH32 (deps/xxhash/xxhash.c) of header names and values, as the reference
  * computes it for every header it encodes (lsqpack.c:1681-1685) or decodes

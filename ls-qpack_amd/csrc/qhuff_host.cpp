@@ -526,6 +526,113 @@ qhuff_decode_batch_host(qhuff_ctx *c, const uint8_t *in,
     return host_batch(c, false, in, in_off, n, 0, out, out_off, status);
 }
 
+// ---- batched literal decode (pre-parsed spans, qhuff_frames.cpp) -----------
+
+extern "C" uint64_t
+qhuff_literals_bound(const struct qhuff_literal *lits, uint32_t n)
+{
+    uint64_t b = 16;
+    for (uint32_t i = 0; lits && i < n; ++i)
+        b += lits[i].huffman ? (uint64_t) lits[i].len * 8 / 5 : lits[i].len;
+    return b;
+}
+
+// Huffman payloads gathered straight into the pinned stage (one copy), one
+// decode launch for all of them, raw literals copied on the host meanwhile.
+// Stage layout: [huff bytes | in_off | out bytes | out_off | status].
+extern "C" int
+qhuff_decode_literals_host(qhuff_ctx *c, const uint8_t *buf,
+                           const struct qhuff_literal *lits, uint32_t n,
+                           uint8_t *out, uint32_t *out_off, uint8_t *status)
+{
+    if (!c || !out_off || (n && (!buf || !lits || !out || !status)))
+        return QHUFF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    uint64_t hb = 0;
+    uint32_t nh = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (lits[i].huffman)
+        {
+            hb += lits[i].len;
+            ++nh;
+        }
+    const uint64_t ob = qhuff_decode_bound(hb, nh);
+    if (ob > 0xffffffffull || hb > 0xffffffffull)
+        return QHUFF_ERANGE;
+    const size_t o_off = up16(hb), o_out = o_off + up16(4ull * (nh + 1));
+    const size_t o_oo = o_out + up16(ob), o_st = o_oo + up16(4ull * (nh + 1));
+    const size_t total = o_st + up16(nh ? nh : 1);
+    int rc = ensure_stage(c, total);
+    if (rc)
+        return rc;
+    hipStream_t st = c->own_stream;
+    uint32_t *hoff = (uint32_t *) (c->h_stage + o_off);
+    {
+        uint32_t k = 0, a = 0;
+        for (uint32_t i = 0; i < n; ++i)
+            if (lits[i].huffman)
+            {
+                memcpy(c->h_stage + a, buf + lits[i].pos, lits[i].len);
+                hoff[k++] = a;
+                a += lits[i].len;
+            }
+        hoff[k] = a;
+    }
+    if (nh)
+    {
+        HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, o_out,
+                                 hipMemcpyHostToDevice, st));
+        rc = qhuff_decode_batch(c, c->d_stage, (const uint32_t *) (c->d_stage
+                                + o_off), nh, c->d_stage + o_out,
+                                (uint32_t *) (c->d_stage + o_oo),
+                                c->d_stage + o_st, st);
+        if (rc)
+            return rc;
+        // sizes and status first (small), then exactly the decoded bytes
+        HIPCHK(c, hipMemcpyAsync(c->h_stage + o_oo, c->d_stage + o_oo,
+                                 4ull * (nh + 1), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(c->h_stage + o_st, c->d_stage + o_st, nh,
+                                 hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        const uint32_t dec_total = ((const uint32_t *) (c->h_stage + o_oo))[nh];
+        HIPCHK(c, hipMemcpyAsync(c->h_stage + o_out, c->d_stage + o_out,
+                                 dec_total, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        uint32_t v = 0;
+        HIPCHK(c, hipMemcpy(&v, c->err, 4, hipMemcpyDeviceToHost));
+        if (v)
+        {
+            (void) hipMemset(c->err, 0, 4);
+            snprintf(c->err_msg, sizeof(c->err_msg), "device error %u", v);
+            return QHUFF_EDEVICE;
+        }
+    }
+    const uint32_t *doo = (const uint32_t *) (c->h_stage + o_oo);
+    const uint8_t *dst = c->h_stage + o_st;
+    uint64_t o = 0;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        out_off[i] = (uint32_t) o;
+        if (lits[i].huffman)
+        {
+            const uint32_t a = doo[k], b = doo[k + 1];
+            status[i] = dst[k];
+            memcpy(out + o, c->h_stage + o_out + a, b - a);
+            o += b - a;
+            ++k;
+        }
+        else
+        {
+            status[i] = QHUFF_DEC_OK;
+            memcpy(out + o, buf + lits[i].pos, lits[i].len);
+            o += lits[i].len;
+        }
+    }
+    out_off[n] = (uint32_t) o;
+    return QHUFF_OK;
+}
+
 // ---- per-string mirrors -----------------------------------------------------
 
 extern "C" int

@@ -27,13 +27,26 @@ EXPORTS = (
     "qhuff_huff_decode", "qhuff_last_error", "qhuff_shard_cuts",
     "qhuff_synth_batch", "qhuff_device_error", "qhuff_profile_read",
     "qhuff_xxh32_headers", "qhuff_xxh32_batch",
+    "qhuff_scan_field_section", "qhuff_scan_encoder_stream",
+    "qhuff_literals_bound", "qhuff_decode_literals_host",
+    "qhuff_frame_literal",
 )
+EPROTO, ETRUNC = -71, -61
+LIT_NAME, LIT_VALUE = 1, 2
 
 XXH_SEED = 39378473                       # LSQPACK_XXH_SEED, lsqpack.c:623
 
 
 class QhuffError(RuntimeError):
     pass
+
+
+class Literal(C.Structure):
+    """struct qhuff_literal (include/qhuff.h)"""
+    _fields_ = [("pos", C.c_uint32), ("len", C.c_uint32),
+                ("huffman", C.c_uint8), ("prefix_bits", C.c_uint8),
+                ("kind", C.c_uint8), ("reserved", C.c_uint8),
+                ("instr", C.c_uint32)]
 
 
 class DecodeRetval(C.Structure):
@@ -96,6 +109,23 @@ def lib():
         L.qhuff_xxh32_batch.restype = C.c_int
         L.qhuff_xxh32_batch.argtypes = [vp, vp, u32p, C.c_uint32, C.c_uint32,
                                         u32p, vp]
+        L.qhuff_scan_field_section.restype = C.c_int
+        L.qhuff_scan_field_section.argtypes = [C.c_char_p, C.c_size_t,
+                                               C.c_uint32, vp, C.c_uint32,
+                                               C.POINTER(C.c_uint32)]
+        L.qhuff_scan_encoder_stream.restype = C.c_int
+        L.qhuff_scan_encoder_stream.argtypes = [
+            C.c_char_p, C.c_size_t, C.c_uint32, vp, C.c_uint32,
+            C.POINTER(C.c_uint32), C.POINTER(C.c_size_t)]
+        L.qhuff_literals_bound.restype = C.c_uint64
+        L.qhuff_literals_bound.argtypes = [vp, C.c_uint32]
+        L.qhuff_decode_literals_host.restype = C.c_int
+        L.qhuff_decode_literals_host.argtypes = [vp, vp, vp, C.c_uint32, vp,
+                                                 u32p, vp]
+        L.qhuff_frame_literal.restype = C.c_int
+        L.qhuff_frame_literal.argtypes = [C.c_uint, vp, C.c_size_t,
+                                          C.c_char_p, C.c_uint, C.c_char_p,
+                                          C.c_uint]
         _lib = L
     return _lib
 
@@ -125,6 +155,42 @@ def shard_cuts(in_off, g):
     if rc:
         raise QhuffError("qhuff_shard_cuts: %d" % rc)
     return cuts
+
+
+def _scan(fn, buf, pos_base, *extra):
+    cap = 64
+    while True:
+        lits = (Literal * cap)()
+        n = C.c_uint32()
+        rc = fn(buf, len(buf), pos_base, lits, cap, C.byref(n), *extra)
+        if rc == ERANGE:
+            cap = max(2 * cap, n.value)
+            continue
+        return rc, list(lits[:n.value])
+
+
+def scan_field_section(buf, pos_base=0):
+    """Literals of one encoded field section -> (rc, [Literal])."""
+    return _scan(lib().qhuff_scan_field_section, bytes(buf), pos_base)
+
+
+def scan_encoder_stream(buf, pos_base=0):
+    """Literals of the complete encoder-stream instructions in buf ->
+    (rc, [Literal], consumed bytes)."""
+    consumed = C.c_size_t()
+    rc, lits = _scan(lib().qhuff_scan_encoder_stream, bytes(buf), pos_base,
+                     C.byref(consumed))
+    return rc, lits, consumed.value
+
+
+def frame_literal(prefix_bits, s, huff, first_byte=0, dst_len=1 << 16):
+    """lsqpack_enc_enc_str framing of s given its precomputed Huffman
+    payload (include/qhuff.h qhuff_frame_literal) -> bytes or -1."""
+    buf = C.create_string_buffer(max(dst_len, 1))
+    buf[0] = first_byte
+    r = lib().qhuff_frame_literal(prefix_bits, buf, dst_len, s, len(s), huff,
+                                  len(huff))
+    return r if r < 0 else buf.raw[:r]
 
 
 TOKEN_ALPHABET = b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, "
@@ -294,6 +360,24 @@ class Codec:
                                            _np_ptr(out_off), _np_ptr(status))
         self._check(rc, "qhuff_decode_batch_host")
         return out[:out_off[-1]], out_off, status[:n]
+
+    def decode_literals_host(self, buf, lits):
+        """Decode pre-parsed literals of host buffer buf in one GPU batch ->
+        (list of bytes, status uint8 ndarray)."""
+        import numpy as np
+        n = len(lits)
+        arr = (Literal * max(n, 1))(*lits)
+        src = np.frombuffer(bytes(buf) + b"\0", dtype=np.uint8)
+        cap = int(lib().qhuff_literals_bound(arr, n))
+        out = np.zeros(cap, dtype=np.uint8)
+        out_off = np.zeros(n + 1, dtype=np.uint32)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        rc = lib().qhuff_decode_literals_host(self._ctx, _np_ptr(src), arr, n,
+                                              _np_ptr(out), _np_ptr(out_off),
+                                              _np_ptr(status))
+        self._check(rc, "qhuff_decode_literals_host")
+        return ([out[out_off[i]:out_off[i + 1]].tobytes() for i in range(n)],
+                status[:n])
 
     # per-string mirrors of the reference entry points ----------------------
     def enc_enc_str(self, prefix_bits, s, first_byte=0, dst_len=1 << 20):

@@ -1,0 +1,226 @@
+"""Literal-span pre-parse of QPACK wire data + batched literal decode
+(include/qhuff.h qhuff_scan_* /
+qhuff_decode_literals_host).
+
+CPU: the C scanner in libqhuff.so (host code, no device) finds exactly the
+literals the test-side wire reader (tests/qpack_frames.py) finds in the
+reference-encoded interop streams and the reference's header-block /
+encoder-stream KATs, resumes encoder streams at any split, and rejects what
+lsqpack_dec_int / _int24 reject (lsqpack.c:2372-2460).
+GPU: every literal of those streams decoded in one batch equals the oracle's
+decode and is a name or value of the QIF the reference encoded it from."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import _paths  # noqa: F401
+import oracle_lib as O
+import qpack_frames as Q
+import qhuff
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+STREAMS = ["netbsd", "fb-req", "fb-resp"]
+
+
+def data_file(name):
+    with open(os.path.join(G, "data", name), "rb") as f:
+        return f.read()
+
+
+def expect(lits_py):
+    return [(d["end"] - len(d["payload"]), len(d["payload"]), d["huffman"],
+             d["prefix_bits"]) for d in lits_py]
+
+
+def got(lits):
+    return [(l.pos, l.len, l.huffman, l.prefix_bits) for l in lits]
+
+
+def frames(name):
+    return list(Q.read_interop(data_file(name + ".out.256.100.1")))
+
+
+# ---- CPU: host scanner ------------------------------------------------------
+
+@pytest.mark.parametrize("name", STREAMS)
+def test_scan_matches_wire_reader(name):
+    n_enc = n_sec = 0
+    for sid, payload in frames(name):
+        if sid == 0:
+            rc, lits, used = qhuff.scan_encoder_stream(payload)
+            assert rc == qhuff.OK
+            py = []
+            for kind, info in Q.encoder_stream_instructions(payload):
+                if kind == "insert_nameref":
+                    py.append(info["value"])
+                elif kind == "insert_literal":
+                    py += [info["name"], info["value"]]
+            assert got(lits) == expect(py)
+            n_enc += len(lits)
+        else:
+            rc, lits = qhuff.scan_field_section(payload)
+            try:
+                py = Q.field_section_literals(payload)
+            except Q.Truncated:
+                assert rc == qhuff.ETRUNC
+                continue
+            assert rc == qhuff.OK
+            assert got(lits) == expect(py)
+            assert all(l.kind in (qhuff.LIT_NAME, qhuff.LIT_VALUE)
+                       for l in lits)
+            n_sec += len(lits)
+    assert n_enc + n_sec > 50
+
+
+@pytest.mark.parametrize("name", STREAMS)
+def test_encoder_stream_resumes_at_any_split(name):
+    enc = b"".join(p for sid, p in frames(name) if sid == 0)
+    _, whole, used = qhuff.scan_encoder_stream(enc)
+    rng = random.Random(5)
+    pos, acc = 0, []
+    pending = b""
+    while pos < len(enc) or pending:
+        k = rng.randrange(1, 40)
+        chunk = pending + enc[pos:pos + k]
+        base = pos - len(pending)
+        pos += k
+        rc, lits, c = qhuff.scan_encoder_stream(chunk, base)
+        assert rc == qhuff.OK
+        acc += lits
+        pending = chunk[c:]
+        if pos >= len(enc):
+            break
+    assert got(acc) == got(whole)
+    assert used + len(pending) == len(enc)
+
+
+def test_scan_reference_header_block_kats():
+    kats = json.load(open(os.path.join(G, "kat_header_blocks.json")))
+    for k in kats["header_blocks"]:
+        sec = bytes.fromhex(k["prefix"] + k["header"])
+        rc, lits = qhuff.scan_field_section(sec)
+        assert rc == qhuff.OK, k["source"]
+        assert got(lits) == expect(Q.field_section_literals(sec))
+        rc, lits, used = qhuff.scan_encoder_stream(bytes.fromhex(k["enc"]))
+        assert rc == qhuff.OK and used == len(k["enc"]) // 2
+
+
+def test_scan_reference_enc_stream_kats():
+    kats = json.load(open(os.path.join(G, "kat_enc_stream.json")))
+    for k in kats["enc_stream"]:
+        buf = bytes.fromhex(k["enc_stream"])
+        rc, lits, used = qhuff.scan_encoder_stream(buf)
+        assert rc == qhuff.OK, k["source"]
+        py = []
+        for kind, info in Q.encoder_stream_instructions(buf):
+            if kind == "insert_nameref":
+                py.append(info["value"])
+            elif kind == "insert_literal":
+                py += [info["name"], info["value"]]
+        assert got(lits) == expect(py)
+
+
+def test_scan_rejects_like_the_reference():
+    # 64-bit overflow in the Required Insert Count (lsqpack_dec_int -> -2)
+    assert qhuff.scan_field_section(b"\xff" + b"\xff" * 10 + b"\x01")[0] \
+        == qhuff.EPROTO
+    # a literal length >= 2^24 (lsqpack_dec_int24 -> -2)
+    big = b"\x00\x00" + b"\x51\x7f\x80\x80\x80\x08"
+    assert qhuff.scan_field_section(big)[0] == qhuff.EPROTO
+    # ends inside a literal / inside the prefix
+    assert qhuff.scan_field_section(b"\x00\x00\x5f\x00\x85\xa4\xa9")[0] \
+        == qhuff.ETRUNC
+    assert qhuff.scan_field_section(b"")[0] == qhuff.ETRUNC
+    # an empty field section is a prefix only
+    assert qhuff.scan_field_section(b"\x00\x00") == (qhuff.OK, [])
+    # encoder stream: a partial instruction is left for the next chunk
+    rc, lits, used = qhuff.scan_encoder_stream(b"\xc0\x8b\xf1\xe3")
+    assert rc == qhuff.OK and lits == [] and used == 0
+    # duplicate index >= 2^24
+    assert qhuff.scan_encoder_stream(b"\x1f\xff\xff\xff\x08")[0] \
+        == qhuff.EPROTO
+
+
+# ---- GPU: all literals of the reference streams in one decode batch ---------
+
+@pytest.fixture(scope="module")
+def codec():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test without a GPU")
+    c = qhuff.Codec(0)
+    yield c
+    c.close()
+
+
+def all_literals():
+    """Every complete encoder-stream / field-section literal of the golden
+    streams, scanned into one concatenated buffer (pos_base per frame)."""
+    buf, lits, truth = b"", [], []
+    for name in STREAMS:
+        strs = Q.qif_strings(data_file(name + ".qif"))
+        for sid, payload in frames(name):
+            base = len(buf)
+            buf += payload
+            if sid == 0:
+                rc, ls, _ = qhuff.scan_encoder_stream(payload, base)
+            else:
+                rc, ls = qhuff.scan_field_section(payload, base)
+                if rc == qhuff.ETRUNC:
+                    continue
+            assert rc == qhuff.OK
+            lits += ls
+            truth += [strs] * len(ls)
+    return buf, lits, truth
+
+
+@pytest.mark.gpu
+def test_gpu_decode_all_stream_literals(codec):
+    buf, lits, truth = all_literals()
+    outs, status = codec.decode_literals_host(buf, lits)
+    assert not status.any()
+    n_huff = 0
+    for l, o, strs in zip(lits, outs, truth):
+        payload = buf[l.pos:l.pos + l.len]
+        if l.huffman:
+            st, want = O.huff_decode(payload)
+            assert st == O.OK
+            n_huff += 1
+        else:
+            want = payload
+        assert o == want
+        # fb-resp carries two empty values the QIF text does not show as
+        # such (interop-encode's QIF reader, not the codec)
+        assert o in strs or o == b""
+    assert n_huff > 100
+
+
+@pytest.mark.gpu
+def test_gpu_decode_literals_with_errors(codec):
+    rng = random.Random(11)
+    buf, lits = b"", []
+    for i in range(3000):
+        s = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 40)))
+        if i % 3:
+            s = O.huffman_enc(s[:30]) if i % 5 else s
+        lit = qhuff.Literal(len(buf), len(s), int(i % 3 != 0), 7, 2, 0, 0)
+        buf += s
+        lits.append(lit)
+    outs, status = codec.decode_literals_host(buf, lits)
+    for l, o, st in zip(lits, outs, status):
+        payload = buf[l.pos:l.pos + l.len]
+        if l.huffman:
+            ost, want = O.huff_decode(payload)
+            assert st == (0 if ost == O.OK else 1)
+            assert o == (want if ost == O.OK else b"")
+        else:
+            assert st == 0 and o == payload
+
+
+@pytest.mark.gpu
+def test_gpu_decode_no_literals(codec):
+    outs, status = codec.decode_literals_host(b"", [])
+    assert outs == [] and len(status) == 0
