@@ -1,5 +1,9 @@
-import sys, random
-sys.path.insert(0,'.'); sys.path.insert(0,'..')
+"""Host simulation behind QH_SPLIT (qhuff_decode.hip): how far past a
+mid-string start bit a second decode chain needs to resynchronise with the
+first, over the bench's synthetic strings (test-side oracle tables)."""
+import os, sys
+T = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests")
+sys.path.insert(0, T)
 import oracle_lib as O
 import _paths, qhuff
 codes = {}
