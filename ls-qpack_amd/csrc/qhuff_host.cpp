@@ -9,7 +9,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "qhuff_kernels.h"
 
@@ -24,6 +30,103 @@ struct DevTables
     uint2 enc[257];                      // {code, bits}
     uint16_t sorted[257];
 };
+
+// Host copy workers for the PCIe-inclusive path: a staging memcpy of tens
+// of MB runs at one core's copy rate, so the pinned staging copies (and the
+// out_off rebasing) are split into slices run by a few persistent threads.
+struct CopyPool
+{
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable go, done;
+    std::function<void(unsigned)> job;
+    unsigned slices = 0;
+    std::atomic<unsigned> next{0};
+    unsigned finished = 0;
+    uint64_t gen = 0;
+    bool stop = false;
+
+    explicit CopyPool(unsigned n)
+    {
+        for (unsigned i = 0; i < n; ++i)
+            th.emplace_back([this] { worker(); });
+    }
+    ~CopyPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto &t : th)
+            t.join();
+    }
+    void worker()
+    {
+        uint64_t seen = 0;
+        for (;;)
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            go.wait(lk, [&] { return stop || gen != seen; });
+            if (stop)
+                return;
+            seen = gen;
+            lk.unlock();
+            unsigned k;
+            while ((k = next.fetch_add(1)) < slices)
+            {
+                job(k);
+                std::lock_guard<std::mutex> g(mu);
+                if (++finished == slices)
+                    done.notify_all();
+            }
+        }
+    }
+    // run fn(0 .. n-1) on the workers and the calling thread; returns when
+    // every slice is done
+    void run(unsigned n, std::function<void(unsigned)> fn)
+    {
+        if (n == 0)
+            return;
+        if (th.empty() || n == 1)
+        {
+            for (unsigned k = 0; k < n; ++k)
+                fn(k);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu);
+            job = std::move(fn);
+            slices = n;
+            finished = 0;
+            next.store(0);
+            ++gen;
+        }
+        go.notify_all();
+        unsigned k;
+        while ((k = next.fetch_add(1)) < slices)
+        {
+            job(k);
+            std::lock_guard<std::mutex> g(mu);
+            if (++finished == slices)
+                done.notify_all();
+        }
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return finished == slices; });
+    }
+    // memcpy split into ~1 MB slices
+    void copy(void *dst, const void *src, size_t n)
+    {
+        const size_t sl = 1u << 20;
+        const unsigned k = (unsigned) ((n + sl - 1) / sl);
+        run(k, [=](unsigned i) {
+            const size_t a = (size_t) i * sl, b = a + sl < n ? a + sl : n;
+            memcpy((uint8_t *) dst + a, (const uint8_t *) src + a, b - a);
+        });
+    }
+};
+
+constexpr unsigned kMaxChunks = 16;          // host-path pipeline depth
 
 struct qhuff_ctx
 {
@@ -48,6 +151,11 @@ struct qhuff_ctx
     size_t h_stage_cap;
     uint8_t *d_stage;
     size_t d_stage_cap;
+    // host-path pipeline: copy streams, per-chunk events, copy workers
+    hipStream_t h2d_stream, d2h_stream;
+    hipEvent_t ev_in[kMaxChunks], ev_k[kMaxChunks], ev_out[kMaxChunks];
+    bool pipe_ready;
+    CopyPool *pool;
     char err_msg[256];
 };
 
@@ -176,6 +284,18 @@ qhuff_close(qhuff_ctx *c)
         (void) hipFree(c->prof);
     if (c->own_stream)
         (void) hipStreamDestroy(c->own_stream);
+    if (c->pipe_ready)
+    {
+        (void) hipStreamDestroy(c->h2d_stream);
+        (void) hipStreamDestroy(c->d2h_stream);
+        for (unsigned i = 0; i < kMaxChunks; ++i)
+        {
+            (void) hipEventDestroy(c->ev_in[i]);
+            (void) hipEventDestroy(c->ev_k[i]);
+            (void) hipEventDestroy(c->ev_out[i]);
+        }
+    }
+    delete c->pool;
     delete c;
 }
 
@@ -440,7 +560,40 @@ up16(size_t x)
     return (x + 15) & ~(size_t) 15;
 }
 
-// layout in both stages: [in bytes | in_off | out bytes | out_off | status]
+static int
+pipe_setup(qhuff_ctx *c)
+{
+    if (c->pipe_ready)
+        return QHUFF_OK;
+    HIPCHK(c, hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking));
+    HIPCHK(c, hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
+    for (unsigned i = 0; i < kMaxChunks; ++i)
+    {
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_in[i], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_k[i], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_out[i], hipEventDisableTiming));
+    }
+    unsigned t = 8;
+    if (const char *e = getenv("QHUFF_HOST_THREADS"))
+        t = (unsigned) strtoul(e, nullptr, 0);
+    if (t > 64)
+        t = 64;
+    c->pool = new CopyPool(t > 1 ? t - 1 : 0);   // + the calling thread
+    c->pipe_ready = true;
+    return QHUFF_OK;
+}
+
+// The PCIe-inclusive path as a chunked pipeline.  The batch is cut into K
+// string ranges; per chunk: pinned staging copy (copy workers) -> H2D on the
+// upload stream -> kernel on the context stream (its out_off / status come
+// back on the same stream) -> once the chunk's size is known, D2H of exactly
+// its output bytes on the download stream -> copy out + rebase out_off on
+// the host.  Chunk i's host copies overlap chunk i-1's kernel and transfers.
+// Kernels stay serialised on one stream (one look-back workspace).
+//
+// Stage layout (pinned and device alike): [in bytes | in_off (n + 1) |
+// out: per-chunk bound regions | out_off: n_i + 1 per chunk | status n].
+// The kernels read the original offsets: `in` is passed rebased by -in_off[0].
 static int
 host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
            uint32_t n, unsigned mode, uint8_t *out, uint32_t *out_off,
@@ -449,49 +602,122 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
     if (!c || !in_off || !out_off || (n && (!in || !out)) || (!enc && n && !status))
         return QHUFF_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
+    int rc = pipe_setup(c);
+    if (rc)
+        return rc;
     const uint64_t a0 = in_off[0], in_bytes = (uint64_t) in_off[n] - a0;
-    const uint64_t ob = enc ? qhuff_encode_bound(in_bytes, n, mode)
-                            : qhuff_decode_bound(in_bytes, n);
-    if (ob > 0xffffffffull)
+    // chunks of >= ~2 MB of input, at most kMaxChunks
+    unsigned K = (unsigned) (in_bytes >> 21);
+    K = K < 1 ? 1 : (K > kMaxChunks ? kMaxChunks : K);
+    if (K > n)
+        K = n ? n : 1;
+    uint32_t cut[kMaxChunks + 1];
+    uint64_t ob[kMaxChunks + 1];                 // out region starts
+    ob[0] = 0;
+    for (unsigned i = 0; i <= K; ++i)
+        cut[i] = (uint32_t) ((uint64_t) n * i / K);
+    for (unsigned i = 0; i < K; ++i)
+    {
+        const uint32_t s0 = cut[i], s1 = cut[i + 1];
+        const uint64_t b = (uint64_t) in_off[s1] - in_off[s0];
+        ob[i + 1] = ob[i] + up16(enc ? qhuff_encode_bound(b, s1 - s0, mode)
+                                     : qhuff_decode_bound(b, s1 - s0));
+    }
+    if (ob[K] > 0xffffffffull)
         return QHUFF_ERANGE;
-    size_t o_in = 0, o_off = up16(in_bytes), o_out = o_off + up16(4ull * (n + 1));
-    size_t o_oo = o_out + up16(ob), o_st = o_oo + up16(4ull * (n + 1));
-    size_t total = o_st + up16(n ? n : 1);
-    int rc = ensure_stage(c, total);
+    const size_t o_in = 0, o_off = up16(in_bytes);
+    const size_t o_out = o_off + up16(4ull * (n + 1));
+    const size_t o_oo = o_out + ob[K];
+    const size_t o_st = o_oo + up16(4ull * (n + K));
+    const size_t total = o_st + up16(n ? n : 1);
+    rc = ensure_stage(c, total);
     if (rc)
         return rc;
-    hipStream_t st = c->own_stream;
-    memcpy(c->h_stage + o_in, in + a0, in_bytes);
-    uint32_t *hoff = (uint32_t *) (c->h_stage + o_off);
-    for (uint32_t i = 0; i <= n; ++i)
-        hoff[i] = in_off[i] - (uint32_t) a0;
-    HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, o_out,
-                             hipMemcpyHostToDevice, st));
-    if (enc)
-        rc = qhuff_encode_batch(c, c->d_stage + o_in,
-                                (const uint32_t *) (c->d_stage + o_off), n,
-                                mode, c->d_stage + o_out,
-                                (uint32_t *) (c->d_stage + o_oo), st);
-    else
-        rc = qhuff_decode_batch(c, c->d_stage + o_in,
-                                (const uint32_t *) (c->d_stage + o_off), n,
-                                c->d_stage + o_out,
-                                (uint32_t *) (c->d_stage + o_oo),
-                                c->d_stage + o_st, st);
-    if (rc)
+    uint8_t *H = c->h_stage, *D = c->d_stage;
+    hipStream_t sk = c->own_stream;
+    uint64_t base = 0;                           // output bytes so far
+    uint32_t tot[kMaxChunks];
+
+    auto stage_in = [&](unsigned i) -> int {
+        const uint32_t s0 = cut[i], s1 = cut[i + 1];
+        const uint64_t b0 = in_off[s0] - a0, b1 = in_off[s1] - a0;
+        c->pool->copy(H + o_in + b0, in + a0 + b0, b1 - b0);
+        memcpy(H + o_off + 4ull * s0, in_off + s0, 4ull * (s1 - s0 + 1));
+        HIPCHK(c, hipMemcpyAsync(D + o_in + b0, H + o_in + b0, b1 - b0,
+                                 hipMemcpyHostToDevice, c->h2d_stream));
+        HIPCHK(c, hipMemcpyAsync(D + o_off + 4ull * s0, H + o_off + 4ull * s0,
+                                 4ull * (s1 - s0 + 1), hipMemcpyHostToDevice,
+                                 c->h2d_stream));
+        HIPCHK(c, hipEventRecord(c->ev_in[i], c->h2d_stream));
+        HIPCHK(c, hipStreamWaitEvent(sk, c->ev_in[i], 0));
+        const uint8_t *din = D + o_in - a0;      // kernels see original offsets
+        const uint32_t *doff = (const uint32_t *) (D + o_off) + s0;
+        uint32_t *doo = (uint32_t *) (D + o_oo) + s0 + i;
+        int r = enc ? qhuff_encode_batch(c, din, doff, s1 - s0, mode,
+                                         D + o_out + ob[i], doo, sk)
+                    : qhuff_decode_batch(c, din, doff, s1 - s0,
+                                         D + o_out + ob[i], doo, D + o_st + s0,
+                                         sk);
+        if (r)
+            return r;
+        HIPCHK(c, hipMemcpyAsync(H + o_oo + 4ull * (s0 + i), doo,
+                                 4ull * (s1 - s0 + 1), hipMemcpyDeviceToHost, sk));
+        if (!enc)
+            HIPCHK(c, hipMemcpyAsync(H + o_st + s0, D + o_st + s0, s1 - s0,
+                                     hipMemcpyDeviceToHost, sk));
+        HIPCHK(c, hipEventRecord(c->ev_k[i], sk));
+        return QHUFF_OK;
+    };
+    auto fetch = [&](unsigned i) -> int {
+        HIPCHK(c, hipEventSynchronize(c->ev_k[i]));
+        const uint32_t s1 = cut[i + 1];
+        tot[i] = ((const uint32_t *) (H + o_oo))[s1 + i];
+        HIPCHK(c, hipStreamWaitEvent(c->d2h_stream, c->ev_k[i], 0));
+        if (tot[i])
+            HIPCHK(c, hipMemcpyAsync(H + o_out + ob[i], D + o_out + ob[i],
+                                     tot[i], hipMemcpyDeviceToHost,
+                                     c->d2h_stream));
+        HIPCHK(c, hipEventRecord(c->ev_out[i], c->d2h_stream));
+        return QHUFF_OK;
+    };
+    auto unstage = [&](unsigned i) -> int {
+        HIPCHK(c, hipEventSynchronize(c->ev_out[i]));
+        const uint32_t s0 = cut[i], s1 = cut[i + 1];
+        c->pool->copy(out + base, H + o_out + ob[i], tot[i]);
+        const uint32_t *ho = (const uint32_t *) (H + o_oo) + s0 + i;
+        const uint32_t bs = (uint32_t) base;
+        const uint32_t m = s1 - s0, sl = 1u << 16;
+        c->pool->run((m + sl - 1) / sl, [=](unsigned k) {
+            const uint32_t a = k * sl, b = a + sl < m ? a + sl : m;
+            for (uint32_t j = a; j < b; ++j)
+                out_off[s0 + j] = bs + ho[j];
+        });
+        if (!enc)
+            memcpy(status + s0, H + o_st + s0, m);
+        base += tot[i];
+        return QHUFF_OK;
+    };
+
+    if (n == 0)
+    {
+        out_off[0] = 0;
+        return QHUFF_OK;
+    }
+    for (unsigned i = 0; i < K; ++i)
+    {
+        if ((rc = stage_in(i)))
+            return rc;
+        if (i >= 1 && (rc = fetch(i - 1)))
+            return rc;
+        if (i >= 2 && (rc = unstage(i - 2)))
+            return rc;
+    }
+    if ((rc = fetch(K - 1)))
         return rc;
-    HIPCHK(c, hipMemcpyAsync(c->h_stage + o_oo, c->d_stage + o_oo,
-                             4ull * (n + 1), hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    memcpy(out_off, c->h_stage + o_oo, 4ull * (n + 1));
-    uint64_t ot = out_off[n];
-    size_t tail = enc ? 0 : up16(n);
-    HIPCHK(c, hipMemcpyAsync(c->h_stage + o_out, c->d_stage + o_out, ot,
-                             hipMemcpyDeviceToHost, st));
-    if (!enc && n)
-        HIPCHK(c, hipMemcpyAsync(c->h_stage + o_st, c->d_stage + o_st, tail,
-                                 hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
+    for (unsigned i = K >= 2 ? K - 2 : 0; i < K; ++i)
+        if ((rc = unstage(i)))
+            return rc;
+    out_off[n] = (uint32_t) base;
     {
         uint32_t v = 0;
         HIPCHK(c, hipMemcpy(&v, c->err, 4, hipMemcpyDeviceToHost));
@@ -502,9 +728,6 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
             return QHUFF_EDEVICE;
         }
     }
-    memcpy(out, c->h_stage + o_out, ot);
-    if (!enc && n)
-        memcpy(status, c->h_stage + o_st, n);
     return QHUFF_OK;
 }
 

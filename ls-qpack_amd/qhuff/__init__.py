@@ -332,29 +332,37 @@ class Codec:
         return h[:n]
 
     # host-memory batch calls (numpy) ----------------------------------------
-    def encode_host(self, data, in_off, mode=ENC_PAYLOAD):
+    def encode_host(self, data, in_off, mode=ENC_PAYLOAD, out=None,
+                    out_off=None):
+        """Host buffers in and out (PCIe-inclusive path).  out / out_off may
+        be given (reused, already faulted-in buffers of the bound size)."""
         import numpy as np
         data = np.ascontiguousarray(data, dtype=np.uint8)
         in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
         n = len(in_off) - 1
-        out = np.zeros(encode_bound(int(in_off[-1] - in_off[0]), n, mode),
-                       dtype=np.uint8)
-        out_off = np.zeros(n + 1, dtype=np.uint32)
+        if out is None:
+            out = np.zeros(encode_bound(int(in_off[-1] - in_off[0]), n, mode),
+                           dtype=np.uint8)
+        if out_off is None:
+            out_off = np.zeros(n + 1, dtype=np.uint32)
         rc = lib().qhuff_encode_batch_host(self._ctx, _np_ptr(data),
                                            _np_ptr(in_off), n, mode,
                                            _np_ptr(out), _np_ptr(out_off))
         self._check(rc, "qhuff_encode_batch_host")
         return out[:out_off[-1]], out_off
 
-    def decode_host(self, data, in_off):
+    def decode_host(self, data, in_off, out=None, out_off=None, status=None):
         import numpy as np
         data = np.ascontiguousarray(data, dtype=np.uint8)
         in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
         n = len(in_off) - 1
-        out = np.zeros(decode_bound(int(in_off[-1] - in_off[0]), n),
-                       dtype=np.uint8)
-        out_off = np.zeros(n + 1, dtype=np.uint32)
-        status = np.zeros(max(n, 1), dtype=np.uint8)
+        if out is None:
+            out = np.zeros(decode_bound(int(in_off[-1] - in_off[0]), n),
+                           dtype=np.uint8)
+        if out_off is None:
+            out_off = np.zeros(n + 1, dtype=np.uint32)
+        if status is None:
+            status = np.zeros(max(n, 1), dtype=np.uint8)
         rc = lib().qhuff_decode_batch_host(self._ctx, _np_ptr(data),
                                            _np_ptr(in_off), n, _np_ptr(out),
                                            _np_ptr(out_off), _np_ptr(status))

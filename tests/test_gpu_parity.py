@@ -313,3 +313,28 @@ def test_host_path_and_mirrors(codec):
     st, out, _ = codec.huff_decode(bytes.fromhex("f1e3c2f51531a245cf64df"),
                                    dst_len=4)
     assert st == 2
+
+
+def test_host_path_pipelined_chunks(codec):
+    """Batches large enough for the chunked host pipeline (>= 2 MB per
+    chunk, several chunks), with in_off[0] != 0 and invalid decode inputs."""
+    import qhuff
+    data, off = qhuff.synth_batch(300001, seed=77, max_len=80)
+    pad = 5
+    data2 = np.concatenate([np.full(pad, 0x41, dtype=np.uint8), data])
+    off2 = off + pad
+    for mode in (0, 7):
+        e, eo = codec.encode_host(data2, off2, mode)
+        o, oo = O.encode_batch(data, off, mode)
+        assert np.array_equal(eo, oo) and np.array_equal(e, o)
+    h, ho = O.encode_batch(data, off, 0)
+    h = h.copy()
+    # corrupt every 97th string's last byte (most become invalid padding)
+    for i in range(0, len(ho) - 1, 97):
+        if ho[i + 1] > ho[i]:
+            h[ho[i + 1] - 1] ^= 0x5A
+    d, do, st = codec.decode_host(h, ho)
+    od, odo, ost = O.decode_batch(h, ho)
+    assert np.array_equal(st, ost) and np.array_equal(do, odo)
+    assert np.array_equal(d, od)
+    assert st.sum() > 100
