@@ -244,7 +244,16 @@ def main():
                "payload_gbps": round(hash_bytes / (hash_ms * 1e-3) / 1e9, 2),
                "alg_bytes": hash_alg,
                "roofline_frac": round(hash_alg / (hash_ms * 1e-3) / 1e9
-                                      / HBM_PEAK_GBS, 4)}
+                                      / HBM_PEAK_GBS, 4),
+               "traffic": None}
+    if os.path.exists(args.pmc):
+        try:
+            ent = json.load(open(args.pmc)).get("kernels", {}).get(
+                "qhuff_hash_kernel")
+            if ent and ent.get("n") == hh:
+                hashing["traffic"] = ent.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
 
     host = None
     if args.host_path and rank == 0:

@@ -20,7 +20,11 @@ def per_kernel(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter or "qhuff" not in r["Kernel_Name"]:
                 continue
-            k = "qhuff_encode_kernel" if "encode" in r["Kernel_Name"] else "qhuff_decode_kernel"
+            name = r["Kernel_Name"]
+            k = next((x for x in ("qhuff_encode_kernel", "qhuff_decode_kernel",
+                                  "qhuff_hash_kernel") if x in name), None)
+            if k is None:
+                continue
             key = (k, r["Dispatch_Id"])
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
     out = {}
@@ -38,7 +42,7 @@ def main():
     for k in sorted(set(fetch) | set(write)):
         fb = fetch.get(k, 0.0) * 1024 * 2
         wb = write.get(k, 0.0) * 1024
-        res["kernels"][k] = {"n": n, "fetch_bytes_raw": fetch.get(k, 0.0) * 1024,
+        res["kernels"][k] = {"n": n // 2 if "hash" in k else n, "fetch_bytes_raw": fetch.get(k, 0.0) * 1024,
                              "fetch_bytes": fb, "write_bytes": wb,
                              "hbm_bytes_per_launch": int(fb + wb)}
     json.dump(res, open(outp, "w"), indent=1)
