@@ -17,7 +17,8 @@
 // loads, then each lane walks its own bytes out of LDS (four 32-bit
 // accumulators over 16-byte stripes, then 4-byte and 1-byte tails).  The
 // outputs are fixed-size (two u32 per header), so no scan or look-back is
-// needed and the grid is simply one wave per tile.  HBM-bound: a header
+// needed; waves are persistent (grid = what is resident) and prefetch the
+// next tile's bytes while hashing the current one.  HBM-bound: a header
 // costs its name + value bytes + 8 B of offsets + 8 B of hashes.
 #include "qhuff_kernels.h"
 
@@ -156,58 +157,123 @@ hash_lane(const R &r, bool pairs, uint32_t a, uint32_t m, uint32_t b,
         *h1 = xxh32(r, a, b - a, seed);
 }
 
+// a tile's offsets: lane l holds header/string l's start, name end (pairs)
+// and end; every lane loads (clamped index), so the count is fixed
+struct HashOffs
+{
+    uint32_t a, m, b, cnt;
+
+    __device__ __forceinline__ void load(const QH_GLB uint32_t *off,
+                                         uint64_t t, uint64_t n, bool pairs)
+    {
+        const uint64_t s0 = t * kWT;
+        cnt = (uint32_t) min((uint64_t) kWT, n - s0);
+        const uint32_t k = pairs ? 2 : 1;
+        const uint32_t li = lane_id() < cnt ? lane_id() : cnt - 1;
+        const QH_GLB uint32_t *o = off + s0 * k + k * li;
+        a = o[0];
+        m = o[1];
+        b = pairs ? o[2] : m;
+    }
+    __device__ __forceinline__ uint32_t first() const { return read_lane(a, 0); }
+    __device__ __forceinline__ uint32_t last() const
+    {
+        return read_lane(b, cnt - 1);
+    }
+};
+
+// Persistent waves, software-pipelined like the codec kernels: while tile t
+// is hashed out of LDS, the bytes of tile t + W and the offsets of tile
+// t + 2W are already in flight (W = waves in the grid).
 __global__ __launch_bounds__(64 * kHashWaves) void
 qhuff_hash_kernel(HashArgs a)
 {
     __shared__ HashWave sm[kHashWaves];
     const uint32_t lane = lane_id();
     const uint32_t wv = threadIdx.x >> 6;
-    const uint64_t t = (uint64_t) blockIdx.x * kHashWaves + wv;
-    const uint64_t s0 = t * kWT;
-    if (s0 >= a.n)
+    const uint64_t nt = (a.n + kWT - 1) / kWT;
+    const uint64_t W = (uint64_t) gridDim.x * kHashWaves;
+    uint64_t t = (uint64_t) blockIdx.x * kHashWaves + wv;
+    if (t >= nt)
         return;
-    const uint32_t cnt = (uint32_t) min((uint64_t) kWT, a.n - s0);
-    const uint32_t k = a.pairs ? 2 : 1;             // offsets per header
-    const QH_GLB uint32_t *off = glb(a.off) + s0 * k;
-    const uint32_t li = lane < cnt ? lane : cnt - 1;
-    const uint32_t oa = off[k * li];
-    const uint32_t om = off[k * li + 1];
-    const uint32_t ob = a.pairs ? off[k * li + 2] : om;
-    const uint32_t first = read_lane(oa, 0);
-    const uint32_t last = read_lane(ob, cnt - 1);
-    const Span sp = tile_span(a.in, first, last, kHashCap);
-    uint32_t h1 = 0, h2 = 0;
-    if (sp.staged)
+    const bool pairs = a.pairs != 0;
+    const QH_GLB uint32_t *off = glb(a.off);
+    auto clamp = [&](uint64_t x) { return x < nt ? x : nt - 1; };
+    QH_LDS uint32_t *s = (QH_LDS uint32_t *) sm[wv].s;
+
+    HashOffs o_cur, o_nxt, o_nn;
+    o_cur.load(off, t, a.n, pairs);
+    Span sp_cur = tile_span(a.in, o_cur.first(), o_cur.last(), kHashCap);
+    Chunks<kHashNch> ch;
+    ch.load(sp_cur);
+    o_nxt.load(off, clamp(t + W), a.n, pairs);
+    for (;;)
     {
-        Chunks<kHashNch> ch;
-        ch.load(sp);
-        QH_LDS uint32_t *s = (QH_LDS uint32_t *) sm[wv].s;
-        ch.store<false>((QH_LDS u32x4 *) s, sp.n16);
+        __builtin_amdgcn_s_waitcnt(0x0f70);           // vmcnt(0)
+        if (sp_cur.staged)
+            ch.store<false>((QH_LDS u32x4 *) s, sp_cur.n16);
         wave_sync();
-        // byte index of input offset x in the stage: x - first + skew
-        const uint32_t skew = (uint32_t) ((uintptr_t) (a.in + first) - sp.pa);
-        const HashLds r{s};
-        hash_lane(r, a.pairs, oa - first + skew, om - first + skew,
-                  ob - first + skew, a.seed, &h1, &h2);
-    }
-    else
-    {
-        const HashGlb r{glb(a.in)};
-        hash_lane(r, a.pairs, oa, om, ob, a.seed, &h1, &h2);
-    }
-    if (lane < cnt)
-    {
-        glb(a.h1)[s0 + lane] = h1;
-        if (a.pairs)
-            glb(a.h2)[s0 + lane] = h2;
+        const Span sp_nxt = tile_span(a.in, o_nxt.first(), o_nxt.last(),
+                                      kHashCap);
+        if (t + W < nt)
+            ch.load(sp_nxt);
+        o_nn.load(off, clamp(t + 2 * W), a.n, pairs);
+
+        uint32_t h1 = 0, h2 = 0;
+        const uint32_t first = o_cur.first();
+        if (sp_cur.staged)
+        {
+            // byte index of input offset x in the stage: x - first + skew
+            const uint32_t skew = (uint32_t) ((uintptr_t) (a.in + first)
+                                              - sp_cur.pa);
+            const HashLds r{s};
+            hash_lane(r, pairs, o_cur.a - first + skew, o_cur.m - first + skew,
+                      o_cur.b - first + skew, a.seed, &h1, &h2);
+        }
+        else
+        {
+            const HashGlb r{glb(a.in)};
+            hash_lane(r, pairs, o_cur.a, o_cur.m, o_cur.b, a.seed, &h1, &h2);
+        }
+        const uint64_t s0 = t * kWT;
+        if (lane < o_cur.cnt)
+        {
+            glb(a.h1)[s0 + lane] = h1;
+            if (pairs)
+                glb(a.h2)[s0 + lane] = h2;
+        }
+        wave_sync();
+        t += W;
+        if (t >= nt)
+            break;
+        o_cur = o_nxt;
+        o_nxt = o_nn;
+        sp_cur = sp_nxt;
     }
 }
 
 hipError_t
 launch_hash(const HashArgs &a, hipStream_t st)
 {
+    static int per_cu = 0, n_cu = 0;
+    if (!per_cu)
+    {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) != hipSuccess
+                || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+            return hipErrorInvalidDevice;
+        n_cu = prop.multiProcessorCount;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, qhuff_hash_kernel, 64 * kHashWaves, 0);
+        if (e != hipSuccess)
+            return e;
+        per_cu = per_cu < 1 ? 1 : per_cu;
+    }
     const uint64_t tiles = (a.n + kWT - 1) / kWT;
-    const uint32_t grid = (uint32_t) ((tiles + kHashWaves - 1) / kHashWaves);
+    const uint64_t need = (tiles + kHashWaves - 1) / kHashWaves;
+    const uint64_t cap = (uint64_t) per_cu * n_cu;
+    const uint32_t grid = (uint32_t) (need < cap ? need : cap);
     hipLaunchKernelGGL(qhuff_hash_kernel, dim3(grid), dim3(64 * kHashWaves),
                        0, st, a);
     return hipGetLastError();
