@@ -173,7 +173,9 @@ struct qhuff_literal
     uint8_t  huffman;           /* H bit                                    */
     uint8_t  prefix_bits;       /* 3, 5 or 7: its length prefix             */
     uint8_t  kind;              /* QHUFF_LIT_NAME / QHUFF_LIT_VALUE         */
-    uint8_t  reserved;
+    uint8_t  hdr_len;           /* bytes of H bit + prefixed length: the
+                                   literal's wire bytes are
+                                   [pos - hdr_len, pos + len)                */
     uint32_t instr;             /* pos_base + offset of its instruction     */
 };
 

@@ -91,6 +91,7 @@ literal(Sink &s, const uint8_t **pp, const uint8_t *end, unsigned prefix_bits,
     const uint8_t *p = *pp;
     if (p >= end)
         return -1;
+    const uint8_t *const start = p;
     const unsigned h = (*p >> prefix_bits) & 1;
     uint32_t len;
     const int r = dec_int24(&p, end, prefix_bits, &len);
@@ -106,7 +107,7 @@ literal(Sink &s, const uint8_t **pp, const uint8_t *end, unsigned prefix_bits,
         l.huffman = (uint8_t) h;
         l.prefix_bits = (uint8_t) prefix_bits;
         l.kind = (uint8_t) kind;
-        l.reserved = 0;
+        l.hdr_len = (uint8_t) (p - start);
         l.instr = s.pos_base + instr;
     }
     else

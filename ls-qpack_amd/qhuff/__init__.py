@@ -45,7 +45,7 @@ class Literal(C.Structure):
     """struct qhuff_literal (include/qhuff.h)"""
     _fields_ = [("pos", C.c_uint32), ("len", C.c_uint32),
                 ("huffman", C.c_uint8), ("prefix_bits", C.c_uint8),
-                ("kind", C.c_uint8), ("reserved", C.c_uint8),
+                ("kind", C.c_uint8), ("hdr_len", C.c_uint8),
                 ("instr", C.c_uint32)]
 
 

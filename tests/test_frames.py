@@ -32,11 +32,12 @@ def data_file(name):
 
 def expect(lits_py):
     return [(d["end"] - len(d["payload"]), len(d["payload"]), d["huffman"],
-             d["prefix_bits"]) for d in lits_py]
+             d["prefix_bits"], d["end"] - len(d["payload"]) - d["start"])
+            for d in lits_py]
 
 
 def got(lits):
-    return [(l.pos, l.len, l.huffman, l.prefix_bits) for l in lits]
+    return [(l.pos, l.len, l.huffman, l.prefix_bits, l.hdr_len) for l in lits]
 
 
 def frames(name):
