@@ -13,8 +13,8 @@
 // each lane keeps a 64-bit bit buffer in registers, refilled from the stage
 // one aligned dword at a time (the refill read is independent of the table
 // lookup, so one LDS round trip sits on the per-step dependency chain).  A
-// step looks the top 12 bits up in a window table (up to two symbols of
-// <= 12 bits); codes of 13..30 bits take a canonical length search behind a
+// step looks the top 13 bits up in a window table (up to two symbols of
+// <= 13 bits); codes of 14..30 bits take a canonical length search behind a
 // wave-uniform branch.  While >= 32 real bits remain the step needs no
 // padding or tail logic; the last < 32 bits run a careful epilogue that
 // pads with ones (as huff_decode_fast pads its last window,

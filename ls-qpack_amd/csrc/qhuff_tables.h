@@ -20,7 +20,12 @@
 
 namespace qhuff {
 
-constexpr int kWinBits = 12;
+// decode window width (QH_WIN_BITS): 13 bits = 32 KB of LDS table, one more
+// two-symbol pair (6 + 7 bits) per lookup than 12
+#ifndef QH_WIN_BITS
+#define QH_WIN_BITS 13
+#endif
+constexpr int kWinBits = QH_WIN_BITS;
 constexpr int kWinSize = 1 << kWinBits;
 constexpr int kMaxLong = 16;            // lengths 13..30 that occur (14 used)
 
