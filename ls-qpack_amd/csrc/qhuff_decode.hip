@@ -33,6 +33,12 @@
 #define QH_EMIT_B16 0
 #endif
 
+// 1: held lanes of the LDS main loop read a hold entry (see
+// decode_string_lds); 0: per-lane gating selects
+#ifndef QH_HOLD_ENTRY
+#define QH_HOLD_ENTRY 1
+#endif
+
 // 1: strings of >= QH_SPLIT_MIN bits are decoded as two chains per lane
 // (decode_string_split); 0: one chain per lane (decode_string_lds).
 // Measured on MI355X: correct, but 2.3x SLOWER (dec 221 vs 96 us) -- the
@@ -67,9 +73,13 @@ struct DecWave                       // one wave's private LDS region
     uint8_t sink[16];                // idle second-chain writes land here
 };
 
+// hold entry, one past the window table: c = 0, ns = 0, not a long code
+constexpr uint32_t kHoldIdx = kWinSize;
+constexpr uint32_t kHoldEntry = 1u << 26;
+
 struct DecSmem
 {
-    uint32_t win[kWinSize];
+    uint32_t win[kWinSize + 4];      // + the hold entry
     uint16_t sorted[257];
     DecWave w[kWaves];
 };
@@ -292,6 +302,47 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
     // <= 12 bits leaves >= 20 valid bits, so the step's dependency chain is
     // lookup -> length -> shift -> index, with the refill beside it (after a
     // long code the index is recomputed behind a second uniform branch)
+#if QH_HOLD_ENTRY
+    // a lane with < 32 real bits left looks up the hold entry instead of
+    // its window (c = ns = 0, never a long code), so the step needs no
+    // per-lane gating and the long-code ballot no lane mask
+    uint32_t idx = rem >= 32 ? (uint32_t) (buf >> (64 - kWinBits)) : kHoldIdx;
+    if (__builtin_amdgcn_ballot_w64(rem >= 32))
+    do
+    {
+        uint32_t e = s_win[idx];
+        uint32_t c = (e >> 16) & 15;          // bits of the entry's symbols
+        uint32_t ns = (e >> 24) & 3;          // symbols (0: longer code)
+        const bool any_long = __builtin_amdgcn_ballot_w64(e < (1u << 24)) != 0;
+        if (any_long)
+        {
+            // a code of 14..30 bits (EOS rejects the string, D3 (a))
+            const bool lng = e < (1u << 24);
+            uint32_t L;
+            const uint32_t sym = long_code((uint32_t) (buf >> 32), s_sorted, &L);
+            const bool eos = lng & (sym == 256);
+            e = lng ? sym : e;
+            c = lng ? (eos ? 0u : L) : c;
+            ns = lng ? (eos ? 0u : 1u) : ns;
+            bad |= eos ? 1u : 0u;
+            rem = eos ? 0u : rem;
+        }
+        buf <<= c;
+        idx = (uint32_t) (buf >> (64 - kWinBits));
+        emit(e, ns);
+        bits -= c;
+        rem -= c;
+        const bool need = bits < 32;
+        const uint32_t dd = need ? nx : 0u;
+        buf |= (uint64_t) dd << ((32 - bits) & 31);
+        bits += need ? 32u : 0u;
+        p += need ? 1u : 0u;
+        nx = src[p];
+        if (any_long)
+            idx = (uint32_t) (buf >> (64 - kWinBits));
+        idx = rem >= 32 ? idx : kHoldIdx;
+    } while (__builtin_amdgcn_ballot_w64(rem >= 32));
+#else
     uint32_t idx = (uint32_t) (buf >> (64 - kWinBits));
     if (__builtin_amdgcn_ballot_w64(rem >= 32))
     do
@@ -330,6 +381,8 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         if (any_long)
             idx = (uint32_t) (buf >> (64 - kWinBits));
     } while (__builtin_amdgcn_ballot_w64(rem >= 32));
+
+#endif
 
     // epilogue: the last < 32 bits, padded with ones; D3 tail rule
     bool fin = bad || rem == 0;
@@ -847,6 +900,8 @@ qhuff_decode_kernel(DecArgs a)
         const QH_GLB uint16_t *gs = glb(a.sorted);
         if (tid < 257)
             sm->sorted[tid] = gs[tid];
+        if (tid == 0)
+            sm->win[kHoldIdx] = kHoldEntry;
         clear_next_launch(a.c);
     }
     __syncthreads();                 // the only workgroup barrier
