@@ -338,3 +338,46 @@ def test_host_path_pipelined_chunks(codec):
     assert np.array_equal(st, ost) and np.array_equal(do, odo)
     assert np.array_equal(d, od)
     assert st.sum() > 100
+
+
+def test_config4_full_size_sharded_round_trip(codec):
+    """Config 4 at its full size: 16,777,216 strings (~604 MB) cut into 8
+    byte-balanced shards (qhuff_shard_cuts, the per-GPU split of the 8-GPU
+    run), each shard coded on cuda:0 through the in_off[0] != 0 path.
+    Size-independent properties: the shard outputs stitched with their bases
+    equal the unsharded encode byte for byte, and the unsharded output
+    decodes back to the input with every status OK."""
+    import qhuff
+    n = 1 << 24
+    data, off = qhuff.synth_batch(n, seed=0x5EED)
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(off.view(np.int32)).to(dev)
+    del data
+    full, full_off = codec.encode(d, o, 0)
+    cuts = qhuff.shard_cuts(off, 8)
+    assert cuts[0] == 0 and cuts[-1] == n
+    fo = full_off.to(torch.int64)
+    for k in range(8):
+        s0, s1 = int(cuts[k]), int(cuts[k + 1])
+        m = s1 - s0
+        b = int(off[s1]) - int(off[s0])
+        out = torch.empty(qhuff.encode_bound(b, m, 0), dtype=torch.uint8,
+                          device=dev)
+        oo = torch.empty(m + 1, dtype=torch.int32, device=dev)
+        codec.encode_into(d, o[s0:], m, 0, out, oo)
+        base = int(fo[s0])
+        rel = fo[s0:s1 + 1] - base
+        assert torch.equal(oo.to(torch.int64), rel)
+        tot = int(rel[-1])
+        assert torch.equal(out[:tot], full[base:base + tot])
+        del out, oo
+    torch.cuda.synchronize()
+    assert codec.device_error() == 0
+    huff = full[:int(fo[-1])].contiguous()
+    raw, roff, st = codec.decode(huff, full_off)
+    torch.cuda.synchronize()
+    assert codec.device_error() == 0
+    assert not bool(st.any())
+    assert torch.equal(roff, o)
+    assert torch.equal(raw[:int(off[-1])], d)
