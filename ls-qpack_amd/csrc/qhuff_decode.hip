@@ -39,38 +39,18 @@
 #define QH_HOLD_ENTRY 1
 #endif
 
-// 1: strings of >= QH_SPLIT_MIN bits are decoded as two chains per lane
-// (decode_string_split); 0: one chain per lane (decode_string_lds).
-// Measured on MI355X: correct, but 2.3x SLOWER (dec 221 vs 96 us) -- the
-// static code self-synchronises slowly on header-like text (a host
-// simulation over the bench alphabet: ~50% of split points resync within
-// 32 bits, ~8% never), and one lane that falls back to a single chain
-// holds its whole wave at twice the per-step cost.  Kept off.
-#ifndef QH_SPLIT
-#define QH_SPLIT 0
-#endif
-#ifndef QH_SPLIT_MIN
-#define QH_SPLIT_MIN 200
-#endif
-
 namespace qhuff {
 
 constexpr int kDecInCap = kStageCap;                   // staged input bytes
-// the second chain of a split string marks its symbol boundaries in the
-// first kSyncW bits after its start (one bit each, a u32)
-constexpr uint32_t kSyncW = 32;
-// byte slot of string i: kSlotPad * i + floor(8 * (rs_i - A) / 5) -- an
-// output is at most 8/5 of its input; the pad covers the byte written past
-// the end by the two-byte emitter and, for a split string, the gap between
-// the first chain's bytes and the second chain's region (split_slot_b)
-constexpr int kSlotPad = QH_SPLIT ? 20 : 2;
-constexpr int kArenaBytes = kSlotPad * kWT + 8 * kDecInCap / 5 + 32;
+// byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
+// most 8/5 of its input, plus one byte written past the end by the
+// two-byte emitter
+constexpr int kArenaBytes = 2 * kWT + 8 * kDecInCap / 5 + 32;
 
 struct DecWave                       // one wave's private LDS region
 {
     alignas(16) uint32_t in[kDecInCap / 4];   // BE input dwords; output stage
     alignas(16) uint8_t arena[kArenaBytes];
-    uint8_t sink[16];                // idle second-chain writes land here
 };
 
 // hold entry, one past the window table: c = 0, ns = 0, not a long code
@@ -502,224 +482,6 @@ struct GlobalEmit                            // slow path: byte stores
     }
 };
 
-// ---- two chains per lane ------------------------------------------------
-//
-// The main loop is latency-bound per wave (one window lookup on each step's
-// dependency chain) and a wave runs as long as its longest string.  A string
-// of >= QH_SPLIT_MIN bits is therefore decoded by two chains in the same
-// lane, interleaved in one loop: chain A from its first bit, chain B from
-// the bit h = about half-way in.  B starts at an unknown symbol alignment
-// but the code resynchronises within a few symbols; B records its symbol
-// boundaries in [h, h + kSyncW) as a bitmask.  When A reaches a boundary
-// that B also has, both decodes agree from there on: A stops, and the
-// output is A's bytes up to that boundary followed by B's bytes after it.
-// If A passes h + kSyncW without a common boundary, or B meets the EOS code
-// before A synchronised (it may be a garbage alignment), B is dropped and A
-// decodes the whole string, exactly as decode_string_lds.  The chain that
-// ends the string (B if synchronised, else A) runs the padded epilogue with
-// the D3 tail rule.  Output = (a_len bytes at the slot) + (bytes of B after
-// the sync point, at *b_src) -- compacted by the caller.
-
-struct Chain                                  // one decode chain's state
-{
-    uint64_t buf;                             // MSB = next bit, >= 32 valid
-    uint32_t bits, p, nx, rem, idx, n;
-
-    __device__ __forceinline__ void init(const QH_LDS uint32_t *src,
-                                         uint32_t bit0, uint32_t bitend)
-    {
-        rem = bitend - bit0;
-        const uint32_t i0 = bit0 >> 5, sk = bit0 & 31;
-        const uint64_t ab = ((uint64_t) src[i0] << 32) | src[i0 + 1];
-        buf = ab << sk;
-        bits = 64 - sk;
-        p = i0 + 2;
-        nx = src[p];
-        idx = (uint32_t) (buf >> (64 - kWinBits));
-        n = 0;
-    }
-
-    // one main step, gated by act (held: c = ns = 0, the two byte writes
-    // land at the current end); returns the bits consumed, the symbols
-    // emitted, the first symbol's length and whether the code was EOS
-    __device__ __forceinline__ void
-    step(bool act, const QH_LDS uint32_t *src, const QH_LDS uint32_t *s_win,
-         const QH_LDS uint16_t *s_sorted, QH_LDS uint8_t *slot, uint32_t &c,
-         uint32_t &ns, uint32_t &l0, bool &eos)
-    {
-        uint32_t e = s_win[idx];
-        c = (e >> 16) & 15;
-        ns = (e >> 24) & 3;
-        l0 = (e >> 20) & 15;
-        eos = false;
-        const bool lng = act & (e < (1u << 24));
-        const bool any_long = __builtin_amdgcn_ballot_w64(lng) != 0;
-        if (any_long)
-        {
-            uint32_t L;
-            const uint32_t sym = long_code((uint32_t) (buf >> 32), s_sorted, &L);
-            eos = lng & (sym == 256);
-            e = lng ? sym : e;
-            c = lng ? (eos ? 0u : L) : c;
-            l0 = lng ? L : l0;
-            ns = lng ? (eos ? 0u : 1u) : ns;
-        }
-        c = act ? c : 0u;
-        ns = act ? ns : 0u;
-        buf <<= c;
-        idx = (uint32_t) (buf >> (64 - kWinBits));
-        slot[n] = (uint8_t) e;
-        slot[n + 1] = (uint8_t) (e >> 8);
-        n += ns;
-        bits -= c;
-        rem -= c;
-        const bool need = bits < 32;
-        const uint32_t dd = need ? nx : 0u;
-        buf |= (uint64_t) dd << ((32 - bits) & 31);
-        bits += need ? 32u : 0u;
-        p += need ? 1u : 0u;
-        nx = src[p];
-        if (any_long)
-            idx = (uint32_t) (buf >> (64 - kWinBits));
-    }
-};
-
-// where chain B of a split string writes, relative to the lane's slot: past
-// every byte A can write before it synchronises or gives up (A stops within
-// one <= 30-bit step of h + kSyncW)
-__device__ __forceinline__ uint32_t
-split_slot_b(uint32_t h)
-{
-    return (h + kSyncW + 30) / 5 + 3;
-}
-
-struct SplitOut
-{
-    uint32_t a_len;                  // bytes of the result at the slot
-    uint32_t b_src;                  // arena offset of the rest
-    int n;                           // total bytes, -1 = rejected
-};
-
-__device__ __forceinline__ SplitOut
-decode_string_split(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
-                    const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
-                    QH_LDS uint8_t *arena, uint32_t slot0, QH_LDS uint8_t *sink)
-{
-    const uint32_t len = bitend - bit0;
-    const bool split = len >= QH_SPLIT_MIN;
-    const uint32_t h = split ? (len >> 1) & ~7u : 0u;
-    const uint32_t slot_b = slot0 + split_slot_b(h);
-    QH_LDS uint8_t *const pa = arena + slot0;
-    QH_LDS uint8_t *const pb = split ? arena + slot_b : sink;
-    Chain A, B;
-    A.init(src, bit0, bitend);
-    B.init(src, bit0 + h, bitend);
-    uint32_t dA = 0, dB = 0;                 // bits consumed by A / B
-    uint32_t M = 1;                          // B's boundaries at h + i
-    bool a_bad = false, b_dead = !split, synced = false, fallback = !split;
-    uint32_t a_len = 0, s_rel = 0;
-    bool a_act = A.rem >= 32, b_act = split && B.rem >= 32;
-    if (__builtin_amdgcn_ballot_w64(a_act | b_act))
-    do
-    {
-        uint32_t c, ns, l0;
-        bool eos;
-        // B first: its boundaries up to dB are final when A looks at them
-        B.step(b_act, src, s_win, s_sorted, pb, c, ns, l0, eos);
-        {
-            const uint32_t b1 = dB + l0, b2 = dB + c;
-            M |= (ns == 2 && b1 < kSyncW) ? 1u << b1 : 0u;
-            M |= (ns != 0 && b2 < kSyncW) ? 1u << b2 : 0u;
-            dB += c;
-            b_dead = b_dead | (b_act & eos);
-        }
-        const uint32_t nA0 = A.n;
-        A.step(a_act, src, s_win, s_sorted, pa, c, ns, l0, eos);
-        {
-            a_bad = a_bad | (a_act & eos);
-            // A's boundaries relative to h (negative -> huge -> no match)
-            const uint32_t r1 = dA + l0 - h, r2 = dA + c - h;
-            const bool chk = a_act & !fallback & !b_dead;
-            const bool m1 = chk & (ns == 2) & (r1 < kSyncW) & (r1 <= dB)
-                          & (((M >> (r1 & 31)) & 1) != 0);
-            const bool m2 = chk & (ns != 0) & (r2 < kSyncW) & (r2 <= dB)
-                          & (((M >> (r2 & 31)) & 1) != 0);
-            const bool hit = m1 | m2;
-            a_len = hit ? (m1 ? nA0 + 1 : A.n) : a_len;
-            s_rel = hit ? (m1 ? r1 : r2) : s_rel;
-            synced = synced | hit;
-            dA += c;
-            // gave up: A is past the window, or B died before a sync
-            fallback = fallback | (!synced & ((dA - h < 0x80000000u
-                                               && dA - h >= kSyncW) | b_dead));
-        }
-        a_act = a_act & !synced & !a_bad & (A.rem >= 32);
-        b_act = b_act & !b_dead & !fallback & (B.rem >= 32);
-    } while (__builtin_amdgcn_ballot_w64(a_act | b_act));
-
-    // the chain that ends the string runs the epilogue
-    const bool use_b = synced;
-    bool bad = a_bad | (synced & b_dead);
-    uint64_t buf = use_b ? B.buf : A.buf;
-    uint32_t rem = use_b ? B.rem : A.rem;
-    ArenaEmit emit{use_b ? pb : pa, use_b ? B.n : A.n};
-    bool fin = bad || rem == 0;
-    if (__builtin_amdgcn_ballot_w64(!fin))
-    do
-    {
-        const uint32_t hi = (uint32_t) (buf >> 32);
-        const uint32_t w = hi | (0xffffffffu >> (rem & 31));
-        const uint32_t e = s_win[w >> (32 - kWinBits)];
-        const uint32_t ns = (e >> 24) & 3, ct = (e >> 16) & 15,
-                       l0 = (e >> 20) & 15;
-        const bool two = (ns == 2) & (ct <= rem);
-        uint32_t c = two ? ct : (ns ? l0 : 31u);
-        uint32_t val = e;
-        bool eos = false;
-        if (__builtin_amdgcn_ballot_w64(!fin & (ns == 0) & (rem > kWinBits)))
-        {
-            uint32_t L;
-            const uint32_t sym = long_code(w, s_sorted, &L);
-            const bool lng = (ns == 0) & (rem > kWinBits);
-            c = lng ? L : c;
-            val = lng ? sym : val;
-            eos = lng & (sym == 256);
-        }
-        const bool over = c > rem;
-        const uint32_t ones = 0xffffffffu >> ((32 - rem) & 31);
-        const bool tail_bad = rem >= 8 || (w >> ((32 - rem) & 31)) != ones;
-        const bool live = !fin;
-        bad = bad | (live & ((over & tail_bad) | (!over & eos)));
-        const bool step = live & !over & !eos;
-        const uint32_t nb = step ? (two ? 2u : 1u) : 0u;
-        c = step ? c : 0;
-        emit(val, nb);
-        buf <<= c;
-        rem -= c;
-        fin = fin | over | eos | (rem == 0);
-    } while (__builtin_amdgcn_ballot_w64(!fin));
-
-    SplitOut r;
-    if (use_b)
-    {
-        // B's bytes before the sync point: one per boundary in (h, h+s_rel]
-        const uint32_t below = (2u << s_rel) - 1u;       // s_rel = 31 -> ~0
-        const uint32_t k0 = __builtin_popcount(M & below) - 1;
-        r.a_len = a_len;
-        r.b_src = slot_b + k0;
-        r.n = (int) (a_len + emit.n - k0);
-    }
-    else
-    {
-        r.a_len = emit.n;
-        r.b_src = slot0;
-        r.n = (int) emit.n;
-    }
-    if (bad)
-        r.n = -1;
-    return r;
-}
-
 // arena slot -> stage at byte D (wave-synchronous; other lanes write the
 // neighbouring bytes): bytes up to a dword boundary, whole dwords, tail
 __device__ __forceinline__ void
@@ -746,8 +508,7 @@ compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
 // line (cold), state by value.
 __device__ __noinline__ void
 dec_slow_tile(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
-              uint32_t slot0, uint32_t a_len, uint32_t b_src, Coord c,
-              uint32_t t, uint32_t cnt, TileOffs to,
+              uint32_t slot0, Coord c, uint32_t t, uint32_t cnt, TileOffs to,
               Span sp, uint32_t sz, uint32_t st, uint8_t *out,
               uint32_t *out_off, uint8_t *status, uint64_t n)
 {
@@ -778,14 +539,9 @@ dec_slow_tile(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
     uint8_t *dst = out + base + excl;
     if (sp.staged)
     {
-        // the bytes are in the arena: a_len at the slot, the rest at b_src
         const QH_LDS uint8_t *sa = wv->arena + slot0;
-        const QH_LDS uint8_t *sb = wv->arena + b_src;
-        const uint32_t a = a_len < sz ? a_len : sz;
-        for (uint32_t i = 0; i < a; ++i)
+        for (uint32_t i = 0; i < sz; ++i)
             ((QH_GLB uint8_t *) dst)[i] = sa[i];
-        for (uint32_t i = a; i < sz; ++i)
-            ((QH_GLB uint8_t *) dst)[i] = sb[i - a];
     }
     else if (valid && st == QHUFF_DEC_OK && sz)
     {
@@ -810,7 +566,6 @@ struct DecPolicy
     QH_LDS DecSmem *sm;
     QH_LDS DecWave *wv;
     uint32_t slot0;                  // this lane's arena slot (current tile)
-    uint32_t a_len = 0, b_src = 0;   // split strings: two output segments
 
     __device__ __forceinline__ void stage_in(const Chunks<kChunks> &ch,
                                              const Span &sp, const TileOffs &)
@@ -828,23 +583,8 @@ struct DecPolicy
     {
         const uint32_t lane = lane_id();
         const uint32_t A = to.first();
-        slot0 = kSlotPad * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
+        slot0 = 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
         int r = 0;
-#if QH_SPLIT
-        a_len = 0;
-        b_src = slot0;
-        if (lane < cnt)
-        {
-            const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
-            const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
-            const SplitOut so = decode_string_split(wv->in, 8 * rs, 8 * re,
-                                                    sm->win, sm->sorted,
-                                                    wv->arena, slot0, wv->sink);
-            r = so.n;
-            a_len = r < 0 ? 0u : so.a_len;
-            b_src = so.b_src;
-        }
-#else
         if (lane < cnt)
         {
             const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
@@ -853,25 +593,15 @@ struct DecPolicy
             r = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted,
                                   em);
         }
-#endif
         *sz = r < 0 ? 0u : (uint32_t) r;
         *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
     }
     // arena -> the (dead) input stage, compacted
     __device__ __forceinline__ void emit(uint32_t excl, uint32_t sz, uint32_t)
     {
-#if QH_SPLIT
-        QH_LDS uint8_t *d = (QH_LDS uint8_t *) wv->in + excl;
-        const uint32_t a = a_len < sz ? a_len : sz;
-        if (a)
-            compact_string(wv->arena + slot0, d, a);
-        if (sz > a)
-            compact_string(wv->arena + b_src, d + a, sz - a);
-#else
         if (sz)
             compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
                            sz);
-#endif
     }
 
     __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
@@ -880,9 +610,8 @@ struct DecPolicy
                                               uint32_t *out_off, uint8_t *status,
                                               uint64_t n)
     {
-        dec_slow_tile(in, sm, wv, slot0, QH_SPLIT ? a_len : sz,
-                      QH_SPLIT ? b_src : slot0, c, t, cnt, to, sp, sz, st,
-                      out, out_off, status, n);
+        dec_slow_tile(in, sm, wv, slot0, c, t, cnt, to, sp, sz, st, out,
+                      out_off, status, n);
     }
 };
 

@@ -1,4 +1,5 @@
-"""Host simulation behind QH_SPLIT (qhuff_decode.hip): how far past a
+"""Host simulation behind the split-decode experiment (commit
+4cb124d): how far past a
 mid-string start bit a second decode chain needs to resynchronise with the
 first, over the bench's synthetic strings (test-side oracle tables)."""
 import os, sys
