@@ -606,8 +606,16 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
     if (rc)
         return rc;
     const uint64_t a0 = in_off[0], in_bytes = (uint64_t) in_off[n] - a0;
-    // chunks of >= ~2 MB of input, at most kMaxChunks
-    unsigned K = (unsigned) (in_bytes >> 21);
+    // chunks of >= 2^chunk_shift bytes of input (QHUFF_HOST_CHUNK_SHIFT;
+    // default 8 MB: measured on MI355X, 1M strings, 8 copy threads -- 2 MB
+    // chunks 2.9 / 2.7 ms enc / dec, 4 MB 2.2 / 2.0, 8 MB 1.8 / 1.7, 16 MB
+    // 1.9 / 2.3; tools/host_path_probe.py), at most kMaxChunks
+    static const unsigned chunk_shift = [] {
+        const char *e = getenv("QHUFF_HOST_CHUNK_SHIFT");
+        const unsigned v = e ? (unsigned) strtoul(e, nullptr, 0) : 23u;
+        return v >= 16 && v <= 30 ? v : 23u;
+    }();
+    unsigned K = (unsigned) (in_bytes >> chunk_shift);
     K = K < 1 ? 1 : (K > kMaxChunks ? kMaxChunks : K);
     if (K > n)
         K = n ? n : 1;

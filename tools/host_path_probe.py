@@ -10,8 +10,9 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(threads):
+def child(threads, shift=21):
     os.environ["QHUFF_HOST_THREADS"] = str(threads)
+    os.environ["QHUFF_HOST_CHUNK_SHIFT"] = str(shift)
     sys.path.insert(0, os.path.join(ROOT, "ls-qpack_amd"))
     import numpy as np
     import qhuff
@@ -34,7 +35,7 @@ def child(threads):
         te = min(te, time.perf_counter() - t)
         t = time.perf_counter(); c.decode_host(h, ho, do, doo, dst)
         td = min(td, time.perf_counter() - t)
-    print(json.dumps({"threads": threads, "enc_ms": round(te * 1e3, 3),
+    print(json.dumps({"threads": threads, "chunk_shift": shift, "enc_ms": round(te * 1e3, 3),
                       "dec_ms": round(td * 1e3, 3),
                       "enc_gbps": round(raw / te / 1e9, 2),
                       "dec_gbps": round(raw / td / 1e9, 2)}), flush=True)
@@ -69,8 +70,9 @@ def raw_rates():
 
 if __name__ == "__main__":
     if len(sys.argv) > 1:
-        child(int(sys.argv[1]))
+        child(int(sys.argv[1]), int(sys.argv[2]))
     else:
         raw_rates()
-        for t in (1, 4, 8, 16):
-            subprocess.check_call([sys.executable, __file__, str(t)])
+        for t, sh in ((1, 21), (8, 21), (8, 22), (2, 23), (4, 23), (8, 23),
+                      (4, 24), (8, 24), (4, 25)):
+            subprocess.check_call([sys.executable, __file__, str(t), str(sh)])
