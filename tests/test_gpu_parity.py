@@ -316,10 +316,11 @@ def test_host_path_and_mirrors(codec):
 
 
 def test_host_path_pipelined_chunks(codec):
-    """Batches large enough for the chunked host pipeline (>= 2 MB per
-    chunk, several chunks), with in_off[0] != 0 and invalid decode inputs."""
+    """Batches large enough for the chunked host pipeline (8 MB chunks,
+    several of them), with in_off[0] != 0 and invalid decode inputs."""
     import qhuff
-    data, off = qhuff.synth_batch(300001, seed=77, max_len=80)
+    # ~44 MB of input: several 8 MB pipeline chunks, a ragged last one
+    data, off = qhuff.synth_batch(1000003, seed=77, max_len=80)
     pad = 5
     data2 = np.concatenate([np.full(pad, 0x41, dtype=np.uint8), data])
     off2 = off + pad
