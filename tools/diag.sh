@@ -21,7 +21,7 @@ libs=("$@")
 for lib in "${libs[@]}"; do
     tag=$(basename "$lib" .so)
     QHUFF_LIB=$PWD/$lib timeout -k 10 180 python -u bench.py --steps 30 \
-        --warmup 5 --cpu-seconds 0 > $o/bench_$tag.json 2> $o/bench_$tag.err
+        --warmup 5 --cpu-seconds 0 --no-host-path > $o/bench_$tag.json 2> $o/bench_$tag.err
     rc=$?
     echo "$tag rc=$rc: $(cat $o/bench_$tag.json)"
     fatal $rc && exit $rc
