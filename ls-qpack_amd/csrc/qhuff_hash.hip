@@ -253,30 +253,22 @@ qhuff_hash_kernel(HashArgs a)
 }
 
 hipError_t
-launch_hash(const HashArgs &a, hipStream_t st)
+launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st)
 {
-    static int per_cu = 0, n_cu = 0;
-    if (!per_cu)
-    {
-        int dev = 0;
-        hipDeviceProp_t prop;
-        if (hipGetDevice(&dev) != hipSuccess
-                || hipGetDeviceProperties(&prop, dev) != hipSuccess)
-            return hipErrorInvalidDevice;
-        n_cu = prop.multiProcessorCount;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, qhuff_hash_kernel, 64 * kHashWaves, 0);
-        if (e != hipSuccess)
-            return e;
-        per_cu = per_cu < 1 ? 1 : per_cu;
-    }
     const uint64_t tiles = (a.n + kWT - 1) / kWT;
     const uint64_t need = (tiles + kHashWaves - 1) / kHashWaves;
-    const uint64_t cap = (uint64_t) per_cu * n_cu;
-    const uint32_t grid = (uint32_t) (need < cap ? need : cap);
+    const uint32_t grid = (uint32_t) (need < max_grid ? need : max_grid);
     hipLaunchKernelGGL(qhuff_hash_kernel, dim3(grid), dim3(64 * kHashWaves),
                        0, st, a);
     return hipGetLastError();
+}
+
+hipError_t
+hash_occupancy(int *blocks_per_cu)
+{
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        blocks_per_cu, reinterpret_cast<const void *>(qhuff_hash_kernel),
+        64 * kHashWaves, 0);
 }
 
 }  // namespace qhuff

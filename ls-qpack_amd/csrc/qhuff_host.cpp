@@ -133,6 +133,7 @@ struct qhuff_ctx
     int device;
     int n_cu;
     uint32_t enc_grid, dec_grid;         // workgroups per launch
+    uint32_t hash_grid;                  // resident hash workgroups
     hipStream_t own_stream;
     DevTables *tab;                      // device
     LongParams lp;
@@ -208,11 +209,13 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     c->lp.n = ht->n_long;
     memcpy(c->lp.l, ht->longc, sizeof(LongLen) * ht->n_long);
     delete ht;
-    int rc, occ_e = 0, occ_d = 0;
+    int rc, occ_e = 0, occ_d = 0, occ_h = 0;
     hipError_t e = encode_occupancy(&occ_e);
     if (e == hipSuccess)
         e = decode_occupancy(&occ_d);
-    if (e != hipSuccess || occ_e < 1 || occ_d < 1)
+    if (e == hipSuccess)
+        e = hash_occupancy(&occ_h);
+    if (e != hipSuccess || occ_e < 1 || occ_d < 1 || occ_h < 1)
     {
         rc = fail(c, e, "occupancy query");
         delete c;
@@ -223,6 +226,7 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     // co-resident: at most the workgroups that fit at once.
     c->enc_grid = (uint32_t) (occ_e * c->n_cu);
     c->dec_grid = (uint32_t) (occ_d * c->n_cu);
+    c->hash_grid = (uint32_t) (occ_h * c->n_cu);
     e = hipMalloc((void **) &c->tab, sizeof(DevTables));
     if (e != hipSuccess)
     {
@@ -508,7 +512,7 @@ hash_call(qhuff_ctx *c, const uint8_t *in, const uint32_t *off, uint32_t n,
     a.n = n;
     a.seed = seed;
     a.pairs = pairs ? 1u : 0u;
-    HIPCHK(c, launch_hash(a, (hipStream_t) stream));
+    HIPCHK(c, launch_hash(a, c->hash_grid, (hipStream_t) stream));
     return QHUFF_OK;
 }
 

@@ -70,7 +70,8 @@ glb(T *p)
 
 hipError_t launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st);
 hipError_t launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st);
-hipError_t launch_hash(const HashArgs &a, hipStream_t st);
+hipError_t launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st);
+hipError_t hash_occupancy(int *blocks_per_cu);
 hipError_t encode_occupancy(int *blocks_per_cu);
 hipError_t decode_occupancy(int *blocks_per_cu);
 size_t encode_lds_bytes();
