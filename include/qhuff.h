@@ -247,6 +247,12 @@ int qhuff_xxh32_batch(qhuff_ctx *ctx, const uint8_t *in,
                       const uint32_t *in_off, uint32_t n, uint32_t seed,
                       uint32_t *hash, void *stream);
 
+/* Host-memory variant of qhuff_xxh32_headers (pinned staging, H2D, kernel,
+ * D2H; synchronous): off is a host array of 2n + 1 offsets into in. */
+int qhuff_xxh32_headers_host(qhuff_ctx *ctx, const uint8_t *in,
+                             const uint32_t *off, uint32_t n, uint32_t seed,
+                             uint32_t *name_hash, uint32_t *nameval_hash);
+
 /* Last HIP error string for this context (diagnostics). */
 const char *qhuff_last_error(qhuff_ctx *ctx);
 

@@ -868,6 +868,48 @@ qhuff_decode_literals_host(qhuff_ctx *c, const uint8_t *buf,
     return QHUFF_OK;
 }
 
+// ---- header hashing, host buffers ----------------------------------------------
+
+// Stage layout: [name/value bytes | offsets (2n + 1) | name_hash | nameval_hash].
+// The kernel reads the caller's offsets unchanged: `in` is passed rebased by
+// -off[0].
+extern "C" int
+qhuff_xxh32_headers_host(qhuff_ctx *c, const uint8_t *in, const uint32_t *off,
+                         uint32_t n, uint32_t seed, uint32_t *name_hash,
+                         uint32_t *nameval_hash)
+{
+    if (!c || !off || (n && (!in || !name_hash || !nameval_hash)))
+        return QHUFF_EINVAL;
+    if (n > 0x7fffffffu)
+        return QHUFF_ERANGE;
+    if (n == 0)
+        return QHUFF_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t a0 = off[0], bytes = (uint64_t) off[2ull * n] - a0;
+    const size_t o_off = up16(bytes), o_h1 = o_off + up16(4ull * (2ull * n + 1));
+    const size_t o_h2 = o_h1 + up16(4ull * n), total = o_h2 + up16(4ull * n);
+    int rc = ensure_stage(c, total);
+    if (rc)
+        return rc;
+    hipStream_t st = c->own_stream;
+    memcpy(c->h_stage, in + a0, bytes);
+    memcpy(c->h_stage + o_off, off, 4ull * (2ull * n + 1));
+    HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, o_h1,
+                             hipMemcpyHostToDevice, st));
+    rc = qhuff_xxh32_headers(c, c->d_stage - a0,
+                             (const uint32_t *) (c->d_stage + o_off), n, seed,
+                             (uint32_t *) (c->d_stage + o_h1),
+                             (uint32_t *) (c->d_stage + o_h2), st);
+    if (rc)
+        return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_stage + o_h1, c->d_stage + o_h1,
+                             total - o_h1, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    memcpy(name_hash, c->h_stage + o_h1, 4ull * n);
+    memcpy(nameval_hash, c->h_stage + o_h2, 4ull * n);
+    return QHUFF_OK;
+}
+
 // ---- per-string mirrors -----------------------------------------------------
 
 extern "C" int

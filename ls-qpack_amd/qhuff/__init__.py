@@ -29,7 +29,7 @@ EXPORTS = (
     "qhuff_xxh32_headers", "qhuff_xxh32_batch",
     "qhuff_scan_field_section", "qhuff_scan_encoder_stream",
     "qhuff_literals_bound", "qhuff_decode_literals_host",
-    "qhuff_frame_literal",
+    "qhuff_frame_literal", "qhuff_xxh32_headers_host",
 )
 EPROTO, ETRUNC = -71, -61
 LIT_NAME, LIT_VALUE = 1, 2
@@ -122,6 +122,9 @@ def lib():
         L.qhuff_decode_literals_host.restype = C.c_int
         L.qhuff_decode_literals_host.argtypes = [vp, vp, vp, C.c_uint32, vp,
                                                  u32p, vp]
+        L.qhuff_xxh32_headers_host.restype = C.c_int
+        L.qhuff_xxh32_headers_host.argtypes = [vp, vp, u32p, C.c_uint32,
+                                               C.c_uint32, u32p, u32p]
         L.qhuff_frame_literal.restype = C.c_int
         L.qhuff_frame_literal.argtypes = [C.c_uint, vp, C.c_size_t,
                                           C.c_char_p, C.c_uint, C.c_char_p,
@@ -318,6 +321,20 @@ class Codec:
         h2 = torch.empty(max(n, 1), dtype=torch.int32, device=data.device)
         self.xxh32_headers_into(data, off, n, seed & 0xffffffff, h1, h2,
                                 stream)
+        return h1[:n], h2[:n]
+
+    def xxh32_headers_host(self, data, off, seed=XXH_SEED):
+        """Host numpy buffers -> (name_hash, nameval_hash) uint32[n]."""
+        import numpy as np
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = (len(off) - 1) // 2
+        h1 = np.zeros(max(n, 1), dtype=np.uint32)
+        h2 = np.zeros(max(n, 1), dtype=np.uint32)
+        rc = lib().qhuff_xxh32_headers_host(self._ctx, _np_ptr(data),
+                                            _np_ptr(off), n, seed & 0xffffffff,
+                                            _np_ptr(h1), _np_ptr(h2))
+        self._check(rc, "qhuff_xxh32_headers_host")
         return h1[:n], h2[:n]
 
     def xxh32(self, data, in_off, seed=XXH_SEED, stream=None):

@@ -157,3 +157,13 @@ def test_gpu_zero_headers(codec):
     g1, g2 = gpu_headers(codec, np.zeros(0, dtype=np.uint8),
                          np.zeros(1, dtype=np.uint32))
     assert len(g1) == 0 and len(g2) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_headers_host_path(codec):
+    pairs, h1, h2 = gold_pairs()
+    data, off = pack_headers(pairs)
+    pad = 7                                     # off[0] != 0
+    data2 = np.concatenate([np.zeros(pad, np.uint8), data])
+    g1, g2 = codec.xxh32_headers_host(data2, off + pad)
+    assert np.array_equal(g1, h1) and np.array_equal(g2, h2)
