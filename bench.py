@@ -32,11 +32,15 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=1 << 20,
                     help="strings per GPU (default 1M)")
     ap.add_argument("--copies", type=int, default=4)
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="bracket the kernels of every E-th timed step with "
+                         "HIP timing events (each timing event costs ~3.6 us "
+                         "of queue time on MI355X; tools/overlap_probe.py)")
     ap.add_argument("--alphabet", default="token", choices=["token", "base64"])
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="wall seconds per CPU-baseline leg (0 = skip)")
@@ -139,8 +143,15 @@ def main():
               and bool((d_st[0] == 0).all())
               and torch.equal(d_ooff[0], d_off[0]))
 
+    # kernel durations for the roofline: HIP events around the kernels of
+    # every E-th timed step (the last of each group of E, so never the first
+    # step after the barrier; the only step when K < E); the rest run
+    # without events
+    ev_every = max(1, min(args.event_every, args.steps))
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
-           for _ in range(args.steps)]
+           if i % ev_every == ev_every - 1 else None
+           for i in range(args.steps)]
+    ev_used = [e for e in evs if e]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -152,8 +163,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     wall = t1 - t0
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev_used) / len(ev_used)
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev_used) / len(ev_used)
 
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
@@ -190,7 +201,8 @@ def main():
             "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": kname, "kernel_us": round(kms * 1e3, 2),
-            "alg_bytes": alg}
+            "alg_bytes": alg,
+            "event_steps": "%d of %d timed steps" % (len(ev_used), args.steps)}
     if pmc_src:
         roof["traffic_source"] = pmc_src
 
