@@ -56,6 +56,18 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_model():
+    """The host CPU model (report it beside the CPU baseline)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def usable_cores():
     try:
         n = len(os.sched_getaffinity(0))
@@ -231,7 +243,8 @@ def main():
                           "lsqpack_enc_enc_str(7,..) + lsqpack_huff_decode "
                           "(fast path), best of %d/%d passes, %d threads"
                           % (n, r1, r2, threads)),
-               "enc_gbps": round(enc_gbs, 3), "dec_gbps": round(dec_gbs, 3)}
+               "enc_gbps": round(enc_gbs, 3), "dec_gbps": round(dec_gbs, 3),
+               "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
 
     # ---- header hashing, outside the timed step --------
     # the batch read as n/2 (name, value) headers: XXH32 name + name/value
