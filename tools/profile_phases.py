@@ -50,14 +50,18 @@ def report(tag, p):
         b = (p[:, :, 5] - p[:, :, 9])[ok]
         print("  emit: emit mean %.0f p90 %.0f | gather+poll mean %.0f p90 %.0f"
               % (a.mean(), np.percentile(a, 90), b.mean(), np.percentile(b, 90)))
-    return
-    # timeline: start of iterations relative to the first stamp
+    if not os.environ.get("TIMELINE"):
+        return
+    # timeline: start of iterations relative to the first stamp (s_memtime
+    # counters; waves on different XCDs may be skewed)
     for it in range(0, ITERS):
         ok = live[:, it]
         if not ok.any():
             break
-        s = p[ok, it, 0] - t0
-        e = p[ok, it, 6] - t0
+        # relative to each wave's own first stamp (counters of different
+        # XCDs are not synchronised)
+        s = p[ok, it, 0] - p[ok, 0, 0]
+        e = p[ok, it, 6] - p[ok, 0, 0]
         e = e[p[ok, it, 6] != 0]
         print("  iter %2d: waves %5d  start p50 %8.0f max %8.0f   end p50 %8.0f max %8.0f"
               % (it, ok.sum(), np.median(s), s.max(),
