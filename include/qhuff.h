@@ -62,8 +62,11 @@ extern "C" {
 typedef struct qhuff_ctx qhuff_ctx;
 
 /* Open a codec context on HIP device `device` (one context per host thread
- * per GPU).  Uploads the static Huffman tables once.  Calls on one context
- * must be ordered on a single stream.  Returns QHUFF_OK or QHUFF_E*. */
+ * per GPU).  Uploads the static Huffman tables once.  A context is not
+ * thread-safe; its launches may use any streams (a launch on another stream
+ * than the context's previous one is ordered after it).  Several contexts
+ * may run on one GPU at once (tiles are claimed in order, so a grid need not
+ * be co-resident).  Returns QHUFF_OK or QHUFF_E*. */
 int qhuff_open(int device, qhuff_ctx **ctx_out);
 void qhuff_close(qhuff_ctx *ctx);
 
@@ -257,9 +260,14 @@ int qhuff_xxh32_headers_host(qhuff_ctx *ctx, const uint8_t *in,
 const char *qhuff_last_error(qhuff_ctx *ctx);
 
 /* Synchronise the device and return (then clear) the context's sticky device
- * error word: 0 = no error; QHUFF_DEVERR_SPIN = a look-back wait gave up
- * (outputs of that launch are invalid).  Negative QHUFF_E* on HIP failure. */
+ * error word: 0 = no error; QHUFF_DEVERR_SPIN = a look-back wait gave up;
+ * QHUFF_DEVERR_RANGE = an output offset passed 2^32 (outputs of that launch
+ * are invalid).  Negative QHUFF_E* on HIP failure.  The asynchronous batch
+ * calls also report such an error: the next qhuff_encode_batch /
+ * qhuff_decode_batch on the context returns QHUFF_EDEVICE (and clears it)
+ * once the launch that hit it has completed. */
 #define QHUFF_DEVERR_SPIN 1
+#define QHUFF_DEVERR_RANGE 2
 int qhuff_device_error(qhuff_ctx *ctx);
 
 /* Diagnostic: in a QHUFF_PROFILE build (libqhuff_prof.so) copy up to

@@ -62,6 +62,7 @@ struct DecSmem
     uint32_t win[kWinSize + 4];      // + the hold entry
     uint16_t sorted[257];
     DecWave w[kWaves];
+    uint32_t tk[2];                  // the block's first two tickets
 };
 
 struct DecLds                        // big-endian dwords staged in LDS
@@ -555,7 +556,11 @@ dec_slow_tile(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
         ((QH_GLB uint8_t *) status)[s0 + lane] = (uint8_t) st;
     }
     if (t == c.n_tiles - 1 && lane == 0)
+    {
         ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + total);
+        if (base + total > 0xffffffffull)        // offsets are 32-bit
+            raise_error(c, kErrRange);
+    }
 }
 
 // the decode side of the wave pipeline (qhuff_pipeline.h)
@@ -633,9 +638,14 @@ qhuff_decode_kernel(DecArgs a)
             sm->win[kHoldIdx] = kHoldEntry;
         clear_next_launch(a.c);
     }
+    Tickets tk;
+    tk.init();
+    claim_block_tickets(a.c, tk, sm->tk);
     __syncthreads();                 // the only workgroup barrier
     DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
-    tile_pipeline(pol, a.c, a.in, a.in_off, a.n, a.out, a.out_off, a.status);
+    const uint32_t w = (uint32_t) (tid >> 6);
+    tile_pipeline(pol, a.c, tk, sm->tk[0] + w, sm->tk[1] + w, a.in, a.in_off,
+                  a.n, a.out, a.out_off, a.status);
 }
 
 hipError_t

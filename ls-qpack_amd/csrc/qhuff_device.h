@@ -50,6 +50,21 @@ constexpr uint64_t kAccMask = kAccOne - 1;
 
 // error bits reported through Coord::err
 constexpr uint32_t kErrSpin = 1;            // look-back spin limit hit
+constexpr uint32_t kErrRange = 2;           // output offsets passed 2^32
+
+// Dynamic tile tickets: tiles are claimed in order from kTickGroups counters
+// (one returning atomic per tile; a single counter saturates near 90
+// claims/us on MI355X, MI355X_MICROARCH.md 'dequeue').  Group g (blocks with
+// blockIdx % G == g) claims tiles g, g + G, g + 2G, ... in order, so every
+// tile a look-back waits on is held by a wave that is running: no
+// co-residency assumption.
+#ifndef QH_TICK_GROUPS
+#define QH_TICK_GROUPS 8
+#endif
+constexpr uint32_t kTickGroups = QH_TICK_GROUPS;
+// each counter on its own 256-byte span (u32 stride): atomics to one line
+// serialise in one L2 channel, and every other access of that channel waits
+constexpr uint32_t kTickStride = 64;
 
 struct Coord
 {
@@ -57,11 +72,17 @@ struct Coord
     unsigned long long *flags;              // per-tile look-back flags
     unsigned long long *sflags;             // per-super-tile flags
     unsigned long long *sacc;               // super accumulators [2][cap_super]
+    uint32_t *tick;                         // tile tickets [2][kTickGroups],
+                                            // kTickStride apart
     uint32_t *err;                          // sticky device error word
+    uint32_t *err_host;                     // its pinned host mirror
     uint32_t epoch;                         // launch tag carried in flags
     uint32_t n_tiles;
     uint32_t cap_super;                     // sacc entries per parity
 };
+
+struct Coord;
+__device__ __forceinline__ void raise_error(const Coord &c, uint32_t bits);
 
 __device__ __forceinline__ uint32_t
 lane_id()
@@ -131,6 +152,15 @@ wave_incl_scan(uint32_t v)
     return x;
 }
 
+__device__ __forceinline__ uint32_t
+wave_max(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1)
+        v = max(v, (uint32_t) __shfl_xor((int) v, d, 64));
+    return v;
+}
+
 template <class T>
 __device__ __forceinline__ T
 wave_sum(T v)
@@ -139,6 +169,16 @@ wave_sum(T v)
     for (int d = 32; d >= 1; d >>= 1)
         v += __shfl_xor(v, d, 64);
     return v;
+}
+
+// sets error bits in the sticky device word and in its pinned host mirror
+// (read by the host at the next batch call, qhuff_host.cpp prepare_launch)
+__device__ __forceinline__ void
+raise_error(const Coord &c, uint32_t bits)
+{
+    atomicOr(c.err, bits);
+    __hip_atomic_fetch_or(c.err_host, bits, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // clears the super accumulators of the next launch on the stream (they use
@@ -152,12 +192,56 @@ clear_next_launch(const Coord &c)
          i += gridDim.x * blockDim.x)
         __hip_atomic_store(&c.sacc[(uint64_t) par * c.cap_super + i], 0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x < kTickGroups)
+        __hip_atomic_store(&c.tick[(par * kTickGroups + threadIdx.x) * kTickStride],
+                           0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// Tile tickets.  claim() issues the returning atomic (lane 0) and does not
+// wait for it; tile_of() reads the result (after a vmcnt wait).
+struct Tickets
+{
+    uint32_t g, G;                          // this block's group, group count
+
+    __device__ __forceinline__ void init()
+    {
+        G = gridDim.x < kTickGroups ? gridDim.x : kTickGroups;
+        g = blockIdx.x % G;
+    }
+    __device__ __forceinline__ uint32_t claim(const Coord &c) const
+    {
+        uint32_t k = 0;
+        if (lane_id() == 0)
+            k = __hip_atomic_fetch_add(
+                &c.tick[((c.epoch & 1) * kTickGroups + g) * kTickStride], 1u,
+                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return k;
+    }
+    // claim m tickets at once (one thread; the caller hands them out)
+    __device__ __forceinline__ uint32_t claim_many(const Coord &c,
+                                                   uint32_t m) const
+    {
+        return __hip_atomic_fetch_add(
+            &c.tick[((c.epoch & 1) * kTickGroups + g) * kTickStride], m,
+            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // tile of ticket k (wave-uniform; ~0u past 2^32 tiles)
+    __device__ __forceinline__ uint32_t tile_of_u(uint32_t k) const
+    {
+        const uint64_t t = (uint64_t) k * G + g;
+        return t < 0xffffffffull ? (uint32_t) t : 0xffffffffu;
+    }
+    // tile of a ticket claim()ed by lane 0
+    __device__ __forceinline__ uint32_t tile_of(uint32_t k) const
+    {
+        return tile_of_u(read_lane(k, 0));
+    }
+};
 
 // ---- profile stamps (QHUFF_PROFILE builds only) --------------------------
 // Stamp slot `ph` of iteration `it` of this wave: prof[(gid * kProfIters +
 // it) * kProfSlots + ph] = s_memtime.  Compiled out otherwise.
-constexpr int kProfIters = 16, kProfSlots = 10;
+constexpr int kProfIters = 16, kProfSlots = 12;
 __device__ __forceinline__ void
 prof_value(const Coord &c, uint32_t it, int ph, uint64_t v)
 {
@@ -172,6 +256,20 @@ prof_value(const Coord &c, uint32_t it, int ph, uint64_t v)
     (void) it;
     (void) ph;
     (void) v;
+#endif
+}
+
+// s_memrealtime (100 MHz) into slot ph: with s_memtime stamps it gives the
+// shader clock the kernel ran at (MI355X_MICROARCH.md, DVFS item 6)
+__device__ __forceinline__ void
+prof_realtime(const Coord &c, uint32_t it, int ph)
+{
+#ifdef QHUFF_PROFILE
+    prof_value(c, it, ph, __builtin_amdgcn_s_memrealtime());
+#else
+    (void) c;
+    (void) it;
+    (void) ph;
 #endif
 }
 
@@ -314,19 +412,24 @@ struct LookBack
         const uint32_t nq = tile - s * kSuper;
         // lanes past the super start re-read the nearest valid slot
         const uint32_t q = lane < nq ? lane : (nq ? nq - 1 : 0);
-        const uint64_t f = __hip_atomic_load(&c.flags[nq ? tile - 1 - q : tile],
-                                             __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        return nq ? f : 0ull;
+        // (the raw flag: finish() masks lanes past nq; no use of the loaded
+        // value here, so the poll's latency is not waited for until then)
+        return __hip_atomic_load(&c.flags[nq ? tile - 1 - q : tile],
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // super flags s-1-lane-64*back (before super 0: inclusive 0)
+    // super flags s-1-lane-64*back, raw (see super_val)
     __device__ __forceinline__ uint64_t poll_super(const Coord &c,
                                                    uint32_t back) const
     {
         const int64_t j = (int64_t) s - 1 - lane_id() - 64 * (int64_t) back;
-        const uint64_t f = __hip_atomic_load(&c.sflags[j < 0 ? 0 : j],
-                                             __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
+        return __hip_atomic_load(&c.sflags[j < 0 ? 0 : j], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // a polled super flag; before super 0: inclusive 0
+    __device__ __forceinline__ uint64_t super_val(const Coord &c, uint32_t back,
+                                                  uint64_t f) const
+    {
+        const int64_t j = (int64_t) s - 1 - lane_id() - 64 * (int64_t) back;
         return j < 0 ? (kFlagInc | ep(c)) : f;
     }
 
@@ -375,7 +478,7 @@ struct LookBack
         if (++*spins > kSpinLimit)
         {
             if (lane_id() == 0)
-                atomicOr(c.err, kErrSpin);
+                raise_error(c, kErrSpin);
             return false;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -418,14 +521,15 @@ struct LookBack
         // 2. super tiles before this one, back to an inclusive one
         for (uint32_t back = 0; !done;)
         {
-            const bool v = flag_valid(fs, c.epoch);
+            const uint64_t fv = super_val(c, back, fs);
+            const bool v = flag_valid(fv, c.epoch);
             const uint64_t inv = __ballot(!v);
-            const uint64_t inc = __ballot(v && flag_inc(fs));
+            const uint64_t inc = __ballot(v && flag_inc(fv));
             const int G = inc ? __builtin_ctzll(inc) : 64;
             const uint64_t upto = G >= 63 ? ~0ull : ((2ull << G) - 1);
             if ((inv & upto) == 0)
             {
-                excl += wave_sum((int) lane <= G ? (fs & kValMask) : 0ull);
+                excl += wave_sum((int) lane <= G ? (fv & kValMask) : 0ull);
                 if (inc)
                     break;
                 fs = poll_super(c, ++back);

@@ -54,6 +54,7 @@ struct EncSmem
                                      // 31 << 27 for longer codes
     uint8_t len[256];
     EncWave w[kWaves];
+    uint32_t tk[2];                  // the block's first two tickets
 };
 
 // source of aligned input dwords: LDS stage or global
@@ -661,7 +662,11 @@ enc_slow_tile(const uint8_t *in, uint32_t mode, QH_LDS EncSmem *sm,
     if (valid)
         ((QH_GLB uint32_t *) out_off)[s0 + lane] = (uint32_t) (base + excl);
     if (t == c.n_tiles - 1 && lane == 0)
+    {
         ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + total);
+        if (base + total > 0xffffffffull)        // offsets are 32-bit
+            raise_error(c, kErrRange);
+    }
 }
 
 // the encode side of the wave pipeline (qhuff_pipeline.h)
@@ -771,6 +776,9 @@ qhuff_encode_kernel(EncArgs a)
     const int tid = threadIdx.x;
     enc_tables_load(sm, a.enc, tid);
     clear_next_launch(a.c);
+    Tickets tk;
+    tk.init();
+    claim_block_tickets(a.c, tk, sm->tk);
     __syncthreads();                 // the only workgroup barrier
     EncPolicy pol;
     pol.in = a.in;
@@ -778,7 +786,9 @@ qhuff_encode_kernel(EncArgs a)
     pol.sm = sm;
     pol.wv = &sm->w[tid >> 6];
     pol.dense = false;
-    tile_pipeline(pol, a.c, a.in, a.in_off, a.n, a.out, a.out_off, nullptr);
+    const uint32_t w = (uint32_t) (tid >> 6);
+    tile_pipeline(pol, a.c, tk, sm->tk[0] + w, sm->tk[1] + w, a.in, a.in_off,
+                  a.n, a.out, a.out_off, nullptr);
 }
 
 hipError_t

@@ -43,6 +43,7 @@ struct CopyPool
     unsigned slices = 0;
     std::atomic<unsigned> next{0};
     unsigned finished = 0;
+    unsigned active = 0;                 // workers inside a claim loop
     uint64_t gen = 0;
     bool stop = false;
 
@@ -71,15 +72,19 @@ struct CopyPool
             if (stop)
                 return;
             seen = gen;
+            ++active;
+            const unsigned ns = slices;
             lk.unlock();
             unsigned k;
-            while ((k = next.fetch_add(1)) < slices)
+            while ((k = next.fetch_add(1)) < ns)
             {
                 job(k);
                 std::lock_guard<std::mutex> g(mu);
-                if (++finished == slices)
-                    done.notify_all();
+                ++finished;
             }
+            std::lock_guard<std::mutex> g(mu);
+            --active;
+            done.notify_all();
         }
     }
     // run fn(0 .. n-1) on the workers and the calling thread; returns when
@@ -104,15 +109,17 @@ struct CopyPool
         }
         go.notify_all();
         unsigned k;
-        while ((k = next.fetch_add(1)) < slices)
+        while ((k = next.fetch_add(1)) < n)
         {
             job(k);
             std::lock_guard<std::mutex> g(mu);
-            if (++finished == slices)
-                done.notify_all();
+            ++finished;
         }
+        // every slice done AND no worker still inside its claim loop: a
+        // straggler's late fetch_add can then not race the next run()'s
+        // reset of job / slices / next (it reads `ns`, its own copy)
         std::unique_lock<std::mutex> lk(mu);
-        done.wait(lk, [&] { return finished == slices; });
+        done.wait(lk, [&] { return finished == n && active == 0; });
     }
     // memcpy split into ~1 MB slices
     void copy(void *dst, const void *src, size_t n)
@@ -157,6 +164,17 @@ struct qhuff_ctx
     hipEvent_t ev_in[kMaxChunks], ev_k[kMaxChunks], ev_out[kMaxChunks];
     bool pipe_ready;
     CopyPool *pool;
+    // launch ordering: every look-back launch records ev_last on its stream;
+    // a launch on another stream waits for it first (one workspace per
+    // context, whichever streams the caller and the host path use)
+    hipEvent_t ev_last;
+    hipStream_t last_stream;
+    bool have_last;
+    // pinned, device-mapped mirror of the device error word: a kernel that
+    // sets an error bit also writes it here, so a batch call reports an
+    // error an earlier (completed) launch left without synchronising
+    uint32_t *err_host;
+    uint32_t *err_host_dev;
     char err_msg[256];
 };
 
@@ -221,9 +239,9 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         delete c;
         return rc ? rc : QHUFF_EDEVICE;
     }
-    // Tiles are assigned statically to the waves of the grid and a
-    // look-back may wait on any earlier tile, so the grid must be
-    // co-resident: at most the workgroups that fit at once.
+    // One launch's grid: the workgroups that fit at once (tiles come from
+    // in-order tickets, so a grid that is not co-resident -- another
+    // context or process on the GPU -- is slower, not wrong).
     c->enc_grid = (uint32_t) (occ_e * c->n_cu);
     c->dec_grid = (uint32_t) (occ_d * c->n_cu);
     c->hash_grid = (uint32_t) (occ_h * c->n_cu);
@@ -241,6 +259,16 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         e = hipMemset(c->err, 0, kErrWords * sizeof(uint32_t));
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipHostMalloc((void **) &c->err_host, 4 * sizeof(uint32_t),
+                          hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess)
+    {
+        memset(c->err_host, 0, 4 * sizeof(uint32_t));
+        e = hipHostGetDevicePointer((void **) &c->err_host_dev, c->err_host, 0);
+    }
     if (e != hipSuccess)
     {
         rc = fail(c, e, "context setup");
@@ -249,8 +277,7 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     }
     c->epoch = 0;
     {
-        // tuning override: fewer workgroups per CU than fit (never more: the
-        // look-back needs the whole grid co-resident)
+        // tuning override: fewer workgroups per CU than fit
         const char *g = getenv("QHUFF_GRID_WG_PER_CU");
         if (g)
         {
@@ -288,6 +315,10 @@ qhuff_close(qhuff_ctx *c)
         (void) hipFree(c->prof);
     if (c->own_stream)
         (void) hipStreamDestroy(c->own_stream);
+    if (c->ev_last)
+        (void) hipEventDestroy(c->ev_last);
+    if (c->err_host)
+        (void) hipHostFree(c->err_host);
     if (c->pipe_ready)
     {
         (void) hipStreamDestroy(c->h2d_stream);
@@ -320,6 +351,8 @@ qhuff_device_error(qhuff_ctx *c)
     HIPCHK(c, hipMemcpy(&v, c->err, 4, hipMemcpyDeviceToHost));
     if (v)
         HIPCHK(c, hipMemset(c->err, 0, 4));
+    v |= c->err_host[0];
+    c->err_host[0] = 0;
     return (int) v;
 }
 
@@ -355,18 +388,41 @@ qhuff_decode_bound(uint64_t in_bytes, uint32_t n)
     return in_bytes * 8 / 5 + 16;
 }
 
+// look-back workspace: the tile tickets [2][kTickGroups] (u32, kTickStride
+// apart), tile flags [cap_tiles], super flags [cap_super], super
+// accumulators [2][cap_super] (u64)
+constexpr size_t kTickBytes = 4 * 2 * kTickGroups * kTickStride;
 static size_t
 lb_bytes(uint64_t cap_tiles, uint64_t cap_super)
 {
-    return 8 * (cap_tiles + 3 * cap_super);
+    return kTickBytes + 8 * (cap_tiles + 3 * cap_super);
 }
 
 // make room for the look-back workspace of `tiles` tiles and advance the
 // epoch (flags are epoch-tagged; the claim counters and super accumulators
-// of a launch are cleared by the launch before it)
+// of a launch are cleared by the launch before it).  Orders the launch
+// after the context's previous one when that ran on another stream, and
+// reports (then clears) a device error a previous launch left behind.
 static int
 prepare_launch(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
 {
+    if (c->err_host[0])
+    {
+        snprintf(c->err_msg, sizeof(c->err_msg),
+                 "device error %u in an earlier launch (outputs invalid)",
+                 c->err_host[0]);
+        c->err_host[0] = 0;
+        (void) hipStreamSynchronize(c->last_stream);
+        (void) hipMemset(c->err, 0, 4);
+        return QHUFF_EDEVICE;
+    }
+    if (c->have_last && st != c->last_stream)
+    {
+        // everything queued on the previous stream so far, our last launch
+        // included, before this one
+        HIPCHK(c, hipEventRecord(c->ev_last, c->last_stream));
+        HIPCHK(c, hipStreamWaitEvent(st, c->ev_last, 0));
+    }
     if (tiles > c->cap_tiles)
     {
         if (c->flags)
@@ -394,6 +450,16 @@ prepare_launch(qhuff_ctx *c, uint64_t tiles, hipStream_t st)
     return QHUFF_OK;
 }
 
+// after a look-back launch on st (the ordering event is recorded only when
+// a later launch comes on another stream, see prepare_launch)
+static int
+finish_launch(qhuff_ctx *c, hipStream_t st)
+{
+    c->last_stream = st;
+    c->have_last = true;
+    return QHUFF_OK;
+}
+
 static Coord
 coord(qhuff_ctx *c, uint64_t tiles)
 {
@@ -409,14 +475,29 @@ coord(qhuff_ctx *c, uint64_t tiles)
         k.prof = c->prof;
     }
 #endif
-    k.flags = c->flags;
-    k.sflags = c->flags + c->cap_tiles;
+    k.tick = (uint32_t *) c->flags;
+    k.flags = c->flags + kTickBytes / 8;
+    k.sflags = k.flags + c->cap_tiles;
     k.sacc = k.sflags + c->cap_super;
     k.cap_super = (uint32_t) c->cap_super;
     k.err = c->err;
+    k.err_host = c->err_host_dev;
     k.epoch = c->epoch;
     k.n_tiles = (uint32_t) tiles;
     return k;
+}
+
+// Workgroups for a launch of `tiles` tiles: tiles are claimed from tickets
+// (any grid size is correct); ticket groups are blockIdx % 8, so a grid of
+// more than 8 blocks is a multiple of 8 (balanced groups), at most `cap`
+// (the co-resident count: more would only queue).
+static uint32_t
+grid_for(uint64_t tiles, uint64_t waves_per_block, uint32_t cap)
+{
+    uint64_t need = (tiles + waves_per_block - 1) / waves_per_block;
+    if (need > kTickGroups)
+        need = (need + kTickGroups - 1) / kTickGroups * kTickGroups;
+    return (uint32_t) (need < cap ? need : cap);
 }
 
 extern "C" int
@@ -449,10 +530,9 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.mode = mode;
     a.c = coord(c, tiles);
     const uint64_t wpb = (uint64_t) encode_waves_per_block();
-    const uint64_t need = (tiles + wpb - 1) / wpb;
-    uint32_t grid = (uint32_t) (need < c->enc_grid ? need : c->enc_grid);
+    const uint32_t grid = grid_for(tiles, wpb, c->enc_grid);
     HIPCHK(c, launch_encode(a, grid, st));
-    return QHUFF_OK;
+    return finish_launch(c, st);
 }
 
 extern "C" int
@@ -485,10 +565,9 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.c = coord(c, tiles);
     a.lp = c->lp;
     const uint64_t wpb = (uint64_t) decode_waves_per_block();
-    const uint64_t need = (tiles + wpb - 1) / wpb;
-    uint32_t grid = (uint32_t) (need < c->dec_grid ? need : c->dec_grid);
+    const uint32_t grid = grid_for(tiles, wpb, c->dec_grid);
     HIPCHK(c, launch_decode(a, grid, st));
-    return QHUFF_OK;
+    return finish_launch(c, st);
 }
 
 // ---- header hashing ---------------------------------------------------------
@@ -733,6 +812,7 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
     {
         uint32_t v = 0;
         HIPCHK(c, hipMemcpy(&v, c->err, 4, hipMemcpyDeviceToHost));
+        c->err_host[0] = 0;              // (this check reports it)
         if (v)
         {
             (void) hipMemset(c->err, 0, 4);
@@ -835,6 +915,7 @@ qhuff_decode_literals_host(qhuff_ctx *c, const uint8_t *buf,
         HIPCHK(c, hipStreamSynchronize(st));
         uint32_t v = 0;
         HIPCHK(c, hipMemcpy(&v, c->err, 4, hipMemcpyDeviceToHost));
+        c->err_host[0] = 0;              // (this check reports it)
         if (v)
         {
             (void) hipMemset(c->err, 0, 4);

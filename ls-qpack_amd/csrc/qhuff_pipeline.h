@@ -1,9 +1,11 @@
 // qhuff_pipeline.h -- the per-wave tile loop shared by the encode and decode
 // kernels (see qhuff_device.h for the execution model).
 //
-// Wave g codes tiles g, g + W, g + 2W, ... (W = waves in the grid; the grid
-// is at most what is co-resident, so every tile a look-back waits on belongs
-// to a running wave).  Per iteration, for tile t:
+// Tiles come from in-order tickets (qhuff_device.h Tickets): a wave's
+// first two tiles from one claim per block in the kernel prologue, then one
+// claim per iteration for the tile two iterations ahead -- every tile a
+// look-back waits on belongs to a running wave, whatever the residency.
+// Per iteration, for tile t:
 //
 //   top    one wait for everything the last iteration issued, a whole codec
 //          ago: t's input chunks and offsets, the older pending tile's
@@ -14,7 +16,8 @@
 //          P::stage_in() -- t's chunks into the LDS stage (the encoder also
 //          runs its byte-parallel pass here, on the chunk registers) -- then
 //          issue the loads of the next tile's input and of the offsets of
-//          the tile after it, so they have the whole codec to land
+//          the tile after it (and the next ticket), so they have the whole
+//          codec to land
 //   codec  P::codec() -- LDS only -- per-lane output size (+ status)
 //   scan   wave scan -> tile-local offsets, tile total; publish the tile
 //          aggregate and add it to the super accumulator (LookBack::start)
@@ -34,12 +37,6 @@
 #include "qhuff_kernels.h"
 
 namespace qhuff {
-
-// 1: the next tile's input / offsets are loaded right after the current
-// tile is staged (a whole codec ahead); 0: after the codec
-#ifndef QH_EARLY_LOADS
-#define QH_EARLY_LOADS 1
-#endif
 
 constexpr int kChunks = 3;                  // 16-byte input chunks per lane
 constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: input / output stage
@@ -74,7 +71,11 @@ flush_tile(const Coord &c, Pending &d, const TileOut<kChunks> &o, uint8_t *out,
             ((QH_GLB uint8_t *) status)[s0 + lane] = (uint8_t) d.stat;
     }
     if (d.tile == c.n_tiles - 1 && lane == 0)
+    {
         ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + d.total);
+        if (base + d.total > 0xffffffffull)      // offsets are 32-bit
+            raise_error(c, kErrRange);
+    }
     d.valid = false;
 }
 
@@ -85,31 +86,56 @@ wait_vm_all()
     __builtin_amdgcn_s_waitcnt(0x0f70);
 }
 
+// The kernel prologue claims each wave's first two tickets for the whole
+// block (one returning atomic per block and claim instead of one per wave:
+// ~3,000 waves claiming at once would queue on the counters)
+// (second-iteration tickets only when the grid's first claims cannot cover
+// every tile: a small batch then gets one tile per wave, not two per wave
+// of the first blocks to start)
+__device__ __forceinline__ void
+claim_block_tickets(const Coord &c, const Tickets &tk, QH_LDS uint32_t *base2)
+{
+    if (threadIdx.x == 0)
+    {
+        base2[0] = tk.claim_many(c, kWaves);
+        base2[1] = (uint64_t) c.n_tiles > (uint64_t) gridDim.x * kWaves
+                 ? tk.claim_many(c, kWaves) : 0xffffffffu / kTickGroups;
+    }
+}
+
 template <class P>
 __device__ __forceinline__ void
-tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_p,
+tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
+              uint32_t k1, const uint8_t *in, const uint32_t *in_off_p,
               uint64_t n, uint8_t *out, uint32_t *out_off, uint8_t *status)
 {
     const QH_GLB uint32_t *in_off = (const QH_GLB uint32_t *) in_off_p;
-    const uint32_t W = gridDim.x * kWaves;
     const uint32_t nt = c.n_tiles;
-    uint32_t t = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    // tiles of this wave's first two iterations (tickets k0 < k1, claimed
+    // for the whole block in the kernel prologue)
+    uint32_t t = tk.tile_of_u(k0);
+    uint32_t tn = tk.tile_of_u(k1);
     if (t >= nt)
         return;
     auto cnt_of = [&](uint32_t tt) -> uint32_t {
         return (uint32_t) min((uint64_t) kWT, n - (uint64_t) tt * kWT);
     };
-    // the tile loads for tile ids past the end read the last tile instead
+    // the loads for tile ids past the end read the last tile instead
     // (fixed instruction counts; the data is never used)
-    auto clamp = [&](uint64_t tt) -> uint32_t {
-        return tt < nt ? (uint32_t) tt : nt - 1;
+    auto clamp = [&](uint32_t tt) -> uint32_t {
+        return tt < nt ? tt : nt - 1;
     };
 
-    // prologue: offsets of t and t + W, input of t (landed at the top)
+    // prologue: offsets of t and tn, input of t (landed at the top), the
+    // ticket of the third iteration
     TileOffs o_cur, o_nxt, o_nn;
     o_cur.load(in_off, (uint64_t) t * kWT, cnt_of(t));
-    const uint32_t tn = clamp((uint64_t) t + W);
-    o_nxt.load(in_off, (uint64_t) tn * kWT, cnt_of(tn));
+    o_nxt.load(in_off, (uint64_t) clamp(tn) * kWT, cnt_of(clamp(tn)));
+    // a wave claims another tile only while its next one is real: a claimed
+    // tile is always coded (tickets of a group are handed out in order, so
+    // once tn is past the end every later claim is too)
+    const uint32_t kNone = 0xffffffffu;
+    uint32_t kq = tn < nt ? tk.claim(c) : kNone;
     Span sp_cur = tile_span(in, o_cur.first(), o_cur.last(), kStageCap);
     Chunks<kChunks> ch;
     ch.load(sp_cur);
@@ -117,21 +143,21 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
     // Two tiles are pending at a time.  Tile k's look-back is resolved at
     // the top of iteration k + 2; its windows are polled at the end of
     // iteration k + 1, a whole codec after every tile before it published
-    // its aggregate (waves start staggered by the dispatch, and a round's
-    // first tiles wait on the previous round's last ones).  Between its
-    // codec and the top of the next iteration a tile's output sits in
-    // registers; then it is parked in the wave's LDS hold buffer -- so no
-    // large register set is live across a codec.
+    // its aggregate.  Tiles come from in-order tickets claimed two
+    // iterations ahead (one claim per wave per iteration), so the order in
+    // which tiles are claimed is the order in which they are coded, and a
+    // look-back only ever waits on tiles held by running waves.  Between its
+    // codec and its store a tile's output sits in registers.
     Pending older, newer;
     older.valid = newer.valid = false;
     TileOut<kChunks> older_out, newer_out;
     uint32_t it = 0;
-    for (uint64_t tile_k = t;; ++it)
+    for (;; ++it)
     {
         prof_stamp(c, it, 0);
         // top: one wait for everything the last iteration issued -- the
         // input of t, offsets, the held tile's polls, the newer tile's
-        // super-accumulator add, the stores of the tile before
+        // super-accumulator add, the stores of the tile before, the ticket
         wait_vm_all();
         prof_stamp(c, it, 1);
         if (newer.valid)
@@ -145,13 +171,14 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
         if (sp_cur.staged)
             pol.stage_in(ch, sp_cur, o_cur);
         wave_sync();
-        // loads for the next tile, a whole codec ahead of their use
+        // loads for the next tiles, a whole codec ahead of their use: input
+        // of tn, offsets of the ticketed tile after it, the next ticket
+        const uint32_t tnn = tn < nt ? tk.tile_of(kq) : kNone;
         const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), kStageCap);
-#if QH_EARLY_LOADS
         ch.load(sp_nxt);
-        const uint32_t tz = clamp(tile_k + 2ull * W);
+        const uint32_t tz = clamp(tnn);
         o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
-#endif
+        kq = tnn < nt ? tk.claim(c) : kNone;
         prof_stamp(c, it, 2);
 
         // codec of t (LDS only when staged)
@@ -165,11 +192,6 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
         const uint32_t total = read_lane(incl, 63);
         fast = fast && total + 64 <= (uint32_t) kStageCap;
         prof_stamp(c, it, 3);
-#if !QH_EARLY_LOADS
-        ch.load(sp_nxt);
-        const uint32_t tz = clamp(tile_k + 2ull * W);
-        o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
-#endif
 
         if (fast)
         {
@@ -203,12 +225,12 @@ tile_pipeline(P &pol, const Coord &c, const uint8_t *in, const uint32_t *in_off_
         wave_sync();
         prof_stamp(c, it, 6);
 
-        tile_k += W;
-        if (tile_k >= nt)
+        if (tn >= nt)
             break;
+        t = tn;
+        tn = tnn;
         o_cur = o_nxt;
         o_nxt = o_nn;
-        t = (uint32_t) tile_k;
         sp_cur = sp_nxt;
     }
     wait_vm_all();

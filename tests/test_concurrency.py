@@ -1,0 +1,99 @@
+"""Forward progress and launch ordering.
+
+* Two contexts on one GPU run full-size (1M-string) launches at the same time
+  on two streams.  Each grid alone fills the GPU, so neither is co-resident
+  while the other runs: tiles come from in-order tickets
+  (qhuff_device.h Tickets), so both finish, bit-exact, with no device error.
+* One context used from two streams (a device-pointer call on a caller
+  stream, then the host path on the context's own stream, no sync between):
+  the launches share one look-back workspace and are ordered by the
+  context's last-launch event.
+"""
+import numpy as np
+import pytest
+
+import _paths  # noqa: F401
+import oracle_lib as O
+
+
+@pytest.fixture(scope="module")
+def batch():
+    import qhuff
+    data, off = qhuff.synth_batch(1 << 20, seed=99)
+    h, ho = O.encode_batch(data, off, 0)
+    return data, off, h, ho
+
+
+def _dev(a, torch):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.gpu
+def test_two_contexts_concurrent_full_size(batch):
+    import torch
+    import qhuff
+    data, off, h, ho = batch
+    c1, c2 = qhuff.Codec(0), qhuff.Codec(0)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    d = _dev(data, torch)
+    o = _dev(off.view(np.int32), torch)
+    hd = _dev(h, torch)
+    hod = _dev(ho.view(np.int32), torch)
+    n = len(off) - 1
+    outs = []
+    torch.cuda.synchronize()
+    for _ in range(3):
+        res = []
+        for c, s in ((c1, s1), (c2, s2)):
+            eo = torch.empty(qhuff.encode_bound(len(data), n, 0),
+                             dtype=torch.uint8, device="cuda")
+            eoo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+            do = torch.empty(qhuff.decode_bound(len(h), n), dtype=torch.uint8,
+                             device="cuda")
+            doo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+            st = torch.empty(n, dtype=torch.uint8, device="cuda")
+            c.encode_into(d, o, n, 0, eo, eoo, s)
+            c.decode_into(hd, hod, n, do, doo, st, s)
+            res.append((eo, eoo, do, doo, st))
+        outs.append(res)
+    torch.cuda.synchronize()
+    assert c1.device_error() == 0 and c2.device_error() == 0
+    for res in outs:
+        for eo, eoo, do, doo, st in res:
+            eoo = eoo.cpu().numpy().view(np.uint32)
+            assert np.array_equal(eoo, ho)
+            assert np.array_equal(eo[:int(eoo[-1])].cpu().numpy(), h)
+            assert np.array_equal(doo.cpu().numpy().view(np.uint32), off)
+            assert not st.cpu().numpy().any()
+            assert np.array_equal(do[:len(data)].cpu().numpy(), data)
+    c1.close()
+    c2.close()
+
+
+@pytest.mark.gpu
+def test_one_context_two_streams(batch):
+    import torch
+    import qhuff
+    data, off, h, ho = batch
+    c = qhuff.Codec(0)
+    s = torch.cuda.Stream()
+    d = _dev(data, torch)
+    o = _dev(off.view(np.int32), torch)
+    n = len(off) - 1
+    torch.cuda.synchronize()
+    for _ in range(2):
+        eo = torch.empty(qhuff.encode_bound(len(data), n, 0), dtype=torch.uint8,
+                         device="cuda")
+        eoo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+        c.encode_into(d, o, n, 0, eo, eoo, s)          # caller stream
+        ho2, hoo2 = c.encode_host(data, off, 0)          # own stream, no sync
+        dr, droo, dst = c.decode_host(h, ho)             # own stream
+        s.synchronize()
+        assert np.array_equal(hoo2, ho) and np.array_equal(ho2, h)
+        assert np.array_equal(droo, off) and not dst.any()
+        assert np.array_equal(dr, data)
+        eoo = eoo.cpu().numpy().view(np.uint32)
+        assert np.array_equal(eoo, ho)
+        assert np.array_equal(eo[:int(eoo[-1])].cpu().numpy(), h)
+    assert c.device_error() == 0
+    c.close()

@@ -16,7 +16,7 @@ import numpy as np
 import torch
 import qhuff
 
-ITERS, SLOTS = 16, 10
+ITERS, SLOTS = 16, 12
 NAMES = ["drain", "flush+park+stage", "codec+scan", "loads+lb.start",
          "emit+gather+poll", "end"]
 
