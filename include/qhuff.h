@@ -144,15 +144,31 @@ struct qhuff_decode_retval
     unsigned                    n_src;
 };
 
-/* lsqpack_huff_decode for a complete string (resume == 0 && final): OK with
- * n_dst/n_src, ERROR with n_dst = n_src = 0 (lsqpack.c:5374-5425), or
- * END_DST with n_dst = n_src = 0 when dst_len is too small (the reference
- * may report partial progress there; callers grow dst and retry either way,
- * lsqpack.c:3327-3365).  Chunked input (final = 0) is not a batch case and
- * returns QHUFF_EINVAL through status ERROR. */
+/* struct lsqpack_decode_status / lsqpack_huff_decode_state (lsqpack.h:
+ * 747-757), same layout */
+struct qhuff_decode_status
+{
+    uint8_t state;
+    uint8_t eos;
+};
+
+struct qhuff_huff_decode_state
+{
+    int                         resume;
+    struct qhuff_decode_status  status;
+};
+
+/* lsqpack_huff_decode(src, src_len, dst, dst_len, state, final)
+ * (lsqpack.c:3524) on context ctx: complete strings (resume == 0 && final)
+ * on the GPU -- OK, ERROR with n_dst = n_src = 0, or END_DST with the
+ * reference's byte-boundary back-off (lsqpack.c:5438-5450) when dst_len is
+ * too small; streaming input through the decoder registered with
+ * qhuff_lsqpack_set_decode_full (qhuff_lsqpack.h, which documents the exact
+ * semantics). */
 struct qhuff_decode_retval
 qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, int src_len,
-                  unsigned char *dst, int dst_len);
+                  unsigned char *dst, int dst_len,
+                  struct qhuff_huff_decode_state *state, int final);
 
 /* ---- literal-span pre-parse + batched literal decode (SURVEY.md 8(f)
  * rank 3).  A host pass walks only the instruction framing of QPACK wire

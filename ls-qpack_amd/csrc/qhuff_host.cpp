@@ -1040,38 +1040,8 @@ qhuff_enc_str_size(qhuff_ctx *c, const unsigned char *str, unsigned str_len)
     return rc == QHUFF_OK ? oo[1] : 0;
 }
 
-extern "C" struct qhuff_decode_retval
-qhuff_huff_decode(qhuff_ctx *c, const unsigned char *src, int src_len,
-                  unsigned char *dst, int dst_len)
-{
-    struct qhuff_decode_retval rv = {QHUFF_HUFF_DEC_ERROR, 0, 0};
-    if (!c || src_len < 0 || dst_len < 0 || (!src && src_len))
-        return rv;
-    uint32_t off[2] = {0, (uint32_t) src_len};
-    uint64_t bound = qhuff_decode_bound((uint64_t) src_len, 1);
-    unsigned char *tmp = (unsigned char *) malloc(bound);
-    unsigned char dummy = 0;
-    uint32_t oo[2] = {0, 0};
-    uint8_t status = QHUFF_DEC_ERROR;
-    if (!tmp)
-        return rv;
-    int rc = qhuff_decode_batch_host(c, src_len ? src : &dummy, off, 1, tmp,
-                                     oo, &status);
-    if (rc == QHUFF_OK && status == QHUFF_DEC_OK)
-    {
-        if (oo[1] <= (uint32_t) dst_len)
-        {
-            memcpy(dst, tmp, oo[1]);
-            rv.status = QHUFF_HUFF_DEC_OK;
-            rv.n_dst = oo[1];
-            rv.n_src = (unsigned) src_len;
-        }
-        else
-            rv.status = QHUFF_HUFF_DEC_END_DST;
-    }
-    free(tmp);
-    return rv;
-}
+// qhuff_huff_decode (lsqpack_huff_decode with its full signature): see
+// qhuff_shim.cpp
 
 // ---- host helpers --------------------------------------------------------------
 

@@ -1,0 +1,174 @@
+// qhuff_shim.cpp -- the reference's per-string entry points with their exact
+// argument lists (include/qhuff_lsqpack.h) and the context form of
+// lsqpack_huff_decode (include/qhuff.h qhuff_huff_decode).
+//
+// A complete string is decoded on the GPU (a one-string batch).  When the
+// caller's dst is too small, or the string holds a code longer than 16 bits,
+// the result the reference reports is a function of where its fast decoder's
+// 16-bit windows fall (huff_decode_fast, lsqpack.c:5243-5466):
+// qhuff_fastwalk.h replays that control flow over the code lengths of the
+// symbols the GPU decoded -- where the output stops, how far it backs off to
+// a byte boundary, or from which byte the reference's nibble decoder takes
+// over.  No bit is decoded on the host.  Streaming input (resume != 0 or final == 0) stays with the
+// reference's own resumable decoder, registered by the integrator
+// (lsqpack_huff_decode_full, lsqpack.c:3443).
+#include <hip/hip_runtime.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <vector>
+
+#include "../../include/qhuff_lsqpack.h"
+#include "qhuff_fastwalk.h"
+#include "qhuff_tables.h"
+
+namespace {
+
+std::atomic<qhuff_huff_decode_full_fn> g_full{nullptr};
+
+// the calling thread's default context (closed at thread exit)
+struct ThreadCtx
+{
+    qhuff_ctx *ctx = nullptr;
+    int device = -1;
+    std::vector<unsigned char> buf;          // one-string decode output
+    std::vector<uint8_t> lens;               // its code lengths
+    ~ThreadCtx()
+    {
+        if (ctx)
+            qhuff_close(ctx);
+    }
+};
+thread_local ThreadCtx t_ctx;
+
+qhuff_ctx *
+default_ctx()
+{
+    if (!t_ctx.ctx)
+    {
+        int dev = t_ctx.device;
+        if (dev < 0)
+        {
+            const char *e = getenv("QHUFF_DEVICE");
+            if (e)
+                dev = atoi(e);
+            else if (hipGetDevice(&dev) != hipSuccess)
+                dev = 0;
+        }
+        if (qhuff_open(dev, &t_ctx.ctx) != QHUFF_OK)
+            t_ctx.ctx = nullptr;
+    }
+    return t_ctx.ctx;
+}
+
+constexpr qhuff_decode_retval kErr = {QHUFF_HUFF_DEC_ERROR, 0, 0};
+
+}  // namespace
+
+extern "C" struct qhuff_decode_retval
+qhuff_huff_decode(qhuff_ctx *c, const unsigned char *src, int src_len,
+                  unsigned char *dst, int dst_len,
+                  struct qhuff_huff_decode_state *state, int final)
+{
+    if (!c || !state || src_len < 0 || dst_len < 0 || (!src && src_len)
+            || (!dst && dst_len))
+        return kErr;
+    if (state->resume != 0 || !final)
+    {
+        const qhuff_huff_decode_full_fn full = g_full.load();
+        return full ? full(src, src_len, dst, dst_len, state, final) : kErr;
+    }
+    // the whole string on the GPU
+    std::vector<unsigned char> &buf = t_ctx.buf;
+    const size_t cap = qhuff_decode_bound((uint64_t) src_len, 1);
+    if (buf.size() < cap)
+        buf.resize(cap);
+    const uint32_t off[2] = {0, (uint32_t) src_len};
+    uint32_t oo[2] = {0, 0};
+    uint8_t st = QHUFF_DEC_ERROR;
+    const unsigned char dummy = 0;
+    if (qhuff_decode_batch_host(c, src_len ? src : &dummy, off, 1, buf.data(),
+                                oo, &st) != QHUFF_OK
+            || st != QHUFF_DEC_OK)
+        return kErr;                         // n_dst = n_src = 0 (5374-5425)
+    const unsigned n = oo[1];
+    // the code lengths decide where the reference's fast decoder stops
+    std::vector<uint8_t> &lens = t_ctx.lens;
+    lens.resize(n);
+    bool has_long = false;
+    for (unsigned i = 0; i < n; ++i)
+    {
+        lens[i] = qhuff::kLen[buf[i]];
+        has_long |= lens[i] > 16;
+    }
+    qhuff::FastStop fs{qhuff::kFastDone, n, (uint32_t) src_len};
+    if (n > (unsigned) dst_len || has_long)
+        fs = qhuff::fast_walk(lens.data(), n, (uint32_t) src_len,
+                              (uint32_t) dst_len);
+    const qhuff_huff_decode_full_fn full = g_full.load();
+    if (fs.end == qhuff::kFastSlow && !full && n <= (unsigned) dst_len)
+        fs = qhuff::FastStop{qhuff::kFastDone, n, (uint32_t) src_len};
+    if (fs.n_dst)
+        memcpy(dst, buf.data(), fs.n_dst);
+    if (fs.end == qhuff::kFastDone)
+        return qhuff_decode_retval{QHUFF_HUFF_DEC_OK, n, (unsigned) src_len};
+    if (fs.end == qhuff::kFastSlow && full)
+    {
+        // the reference finishes with its nibble decoder from that byte
+        // (lsqpack.c:5452-5465)
+        qhuff_decode_retval rv = full(src + fs.n_src, src_len - (int) fs.n_src,
+                                      dst + fs.n_dst, dst_len - (int) fs.n_dst,
+                                      state, final);
+        if (rv.status == QHUFF_HUFF_DEC_OK || rv.status == QHUFF_HUFF_DEC_END_DST)
+        {
+            rv.n_dst += fs.n_dst;
+            rv.n_src += fs.n_src;
+        }
+        return rv;
+    }
+    // dst_ended, or a slow-path stop with no streaming decoder registered
+    return qhuff_decode_retval{QHUFF_HUFF_DEC_END_DST, fs.n_dst, fs.n_src};
+}
+
+extern "C" int
+qhuff_lsqpack_enc_enc_str(unsigned prefix_bits, unsigned char *dst,
+                          size_t dst_len, const unsigned char *str,
+                          unsigned str_len)
+{
+    qhuff_ctx *c = default_ctx();
+    return c ? qhuff_enc_enc_str(c, prefix_bits, dst, dst_len, str, str_len)
+             : -1;
+}
+
+extern "C" struct qhuff_decode_retval
+qhuff_lsqpack_huff_decode(const unsigned char *src, int src_len,
+                          unsigned char *dst, int dst_len,
+                          struct qhuff_huff_decode_state *state, int final)
+{
+    if (state && (state->resume != 0 || !final))
+    {
+        // streaming input never needs the GPU context
+        const qhuff_huff_decode_full_fn full = g_full.load();
+        return full ? full(src, src_len, dst, dst_len, state, final) : kErr;
+    }
+    qhuff_ctx *c = default_ctx();
+    return c ? qhuff_huff_decode(c, src, src_len, dst, dst_len, state, final)
+             : kErr;
+}
+
+extern "C" void
+qhuff_lsqpack_set_decode_full(qhuff_huff_decode_full_fn fn)
+{
+    g_full.store(fn);
+}
+
+extern "C" int
+qhuff_lsqpack_set_device(int device)
+{
+    if (t_ctx.ctx)
+        return QHUFF_EINVAL;
+    t_ctx.device = device;
+    return QHUFF_OK;
+}

@@ -12,6 +12,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)                 # .../ls-qpack_amd
 LIB_PATH = os.environ.get("QHUFF_LIB") or os.path.join(PKG_ROOT, "libqhuff.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "qhuff.h")
+HEADERS = (HEADER, os.path.join(os.path.dirname(PKG_ROOT), "include",
+                                "qhuff_lsqpack.h"))
 
 OK = 0
 EINVAL, ENOMEM, ENODEV, ERANGE, EDEVICE = -22, -12, -19, -34, -5
@@ -30,6 +32,9 @@ EXPORTS = (
     "qhuff_scan_field_section", "qhuff_scan_encoder_stream",
     "qhuff_literals_bound", "qhuff_decode_literals_host",
     "qhuff_frame_literal", "qhuff_xxh32_headers_host",
+    # include/qhuff_lsqpack.h
+    "qhuff_lsqpack_enc_enc_str", "qhuff_lsqpack_huff_decode",
+    "qhuff_lsqpack_set_decode_full", "qhuff_lsqpack_set_device",
 )
 EPROTO, ETRUNC = -71, -61
 LIT_NAME, LIT_VALUE = 1, 2
@@ -50,7 +55,19 @@ class Literal(C.Structure):
 
 
 class DecodeRetval(C.Structure):
+    """struct qhuff_decode_retval (= struct huff_decode_retval,
+    lsqpack.c:3420-3431)"""
     _fields_ = [("status", C.c_int), ("n_dst", C.c_uint), ("n_src", C.c_uint)]
+
+
+class DecodeState(C.Structure):
+    """struct qhuff_huff_decode_state (= struct lsqpack_huff_decode_state,
+    lsqpack.h:747-757)"""
+    _fields_ = [("resume", C.c_int), ("state", C.c_uint8), ("eos", C.c_uint8)]
+
+
+DECODE_FULL_FN = C.CFUNCTYPE(DecodeRetval, C.c_void_p, C.c_int, C.c_void_p,
+                             C.c_int, C.POINTER(DecodeState), C.c_int)
 
 
 _lib = None
@@ -92,7 +109,19 @@ def lib():
         L.qhuff_enc_str_size.restype = C.c_uint
         L.qhuff_enc_str_size.argtypes = [vp, C.c_char_p, C.c_uint]
         L.qhuff_huff_decode.restype = DecodeRetval
-        L.qhuff_huff_decode.argtypes = [vp, C.c_char_p, C.c_int, vp, C.c_int]
+        L.qhuff_huff_decode.argtypes = [vp, vp, C.c_int, vp, C.c_int,
+                                        C.POINTER(DecodeState), C.c_int]
+        L.qhuff_lsqpack_enc_enc_str.restype = C.c_int
+        L.qhuff_lsqpack_enc_enc_str.argtypes = [C.c_uint, vp, C.c_size_t,
+                                                C.c_char_p, C.c_uint]
+        L.qhuff_lsqpack_huff_decode.restype = DecodeRetval
+        L.qhuff_lsqpack_huff_decode.argtypes = [vp, C.c_int, vp, C.c_int,
+                                                C.POINTER(DecodeState),
+                                                C.c_int]
+        L.qhuff_lsqpack_set_decode_full.restype = None
+        L.qhuff_lsqpack_set_decode_full.argtypes = [C.c_void_p]
+        L.qhuff_lsqpack_set_device.restype = C.c_int
+        L.qhuff_lsqpack_set_device.argtypes = [C.c_int]
         L.qhuff_last_error.restype = C.c_char_p
         L.qhuff_last_error.argtypes = [vp]
         L.qhuff_shard_cuts.restype = C.c_int
@@ -210,6 +239,36 @@ def synth_batch(n, seed=0, min_len=8, max_len=64, alphabet=TOKEN_ALPHABET):
     tot = lib().qhuff_synth_batch(seed, n, min_len, max_len, alphabet,
                                   len(alphabet), _np_ptr(data), _np_ptr(off))
     return data[:tot].copy(), off
+
+
+# ---- exact-signature shims (include/qhuff_lsqpack.h) -------------------------
+
+def lsqpack_enc_enc_str(prefix_bits, s, first_byte=0, dst_len=1 << 16):
+    """qhuff_lsqpack_enc_enc_str -> bytes or -1 (thread's default context)."""
+    buf = C.create_string_buffer(max(dst_len, 1))
+    buf[0] = first_byte
+    r = lib().qhuff_lsqpack_enc_enc_str(prefix_bits, buf, dst_len, s, len(s))
+    return r if r < 0 else buf.raw[:r]
+
+
+def lsqpack_huff_decode(src, dst_len, state=None, final=1):
+    """qhuff_lsqpack_huff_decode -> (status, dst[:n_dst], n_dst, n_src,
+    state)."""
+    s = C.create_string_buffer(bytes(src), len(src) + 1)
+    d = C.create_string_buffer(max(dst_len, 1))
+    st = state if state is not None else DecodeState(0, 0, 0)
+    rv = lib().qhuff_lsqpack_huff_decode(s, len(src), d, dst_len, C.byref(st),
+                                         final)
+    return rv.status, d.raw[:rv.n_dst], rv.n_dst, rv.n_src, st
+
+
+def lsqpack_set_decode_full(fn):
+    """Register the streaming decoder (a DECODE_FULL_FN or None); returns
+    the ctypes callback object, which the caller must keep alive."""
+    cb = fn if fn is None or isinstance(fn, DECODE_FULL_FN) else DECODE_FULL_FN(fn)
+    lib().qhuff_lsqpack_set_decode_full(
+        C.cast(cb, C.c_void_p) if cb is not None else None)
+    return cb
 
 
 # ---- device codec ----------------------------------------------------------
@@ -415,9 +474,14 @@ class Codec:
     def enc_str_size(self, s):
         return int(lib().qhuff_enc_str_size(self._ctx, s, len(s)))
 
-    def huff_decode(self, src, dst_len=None):
+    def huff_decode(self, src, dst_len=None, state=None, final=1):
+        """qhuff_huff_decode (lsqpack_huff_decode's arguments on this
+        context) -> (status, dst bytes [:n_dst], n_src)."""
         if dst_len is None:
             dst_len = len(src) * 8 // 5 + 1
+        s = C.create_string_buffer(bytes(src), len(src) + 1)
         d = C.create_string_buffer(max(dst_len, 1))
-        rv = lib().qhuff_huff_decode(self._ctx, src, len(src), d, dst_len)
+        st = state if state is not None else DecodeState(0, 0, 0)
+        rv = lib().qhuff_huff_decode(self._ctx, s, len(src), d, dst_len,
+                                     C.byref(st), final)
         return rv.status, d.raw[:rv.n_dst], rv.n_src
