@@ -28,3 +28,51 @@ def test_hook_demo_round_trips_reference_streams(name):
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "re-framed mismatches 0" in r.stdout
+
+
+# ---- examples/qhuff_hook.c: the INTEGRATION.md section 2 memo + seams ------
+
+HOOK_TEST = os.path.join(ROOT, "tests", "c", "_build", "hook_test")
+
+
+def _build_hook_test():
+    import oracle_lib
+    oracle_lib.build()
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "c")])
+
+
+def test_hook_test_builds_and_links():
+    """qhuff_hook.c compiles as gnu99 -Werror and links libqhuff.so (the
+    test program also links the oracle, as the checker)."""
+    subprocess.check_call(["make", "-s", "-C", EX, "qhuff_hook.o"])
+    _build_hook_test()
+    out = subprocess.check_output(["ldd", HOOK_TEST]).decode()
+    assert "libqhuff.so" in out and "not found" not in out
+
+
+@pytest.mark.gpu
+def test_hook_encoder_seam_matches_lsqpack_enc_enc_str():
+    """Every name and value of the reference's QIF inputs through one memo
+    batch per file: lsqpack_qhuff_enc_lookup == lsqpack_enc_enc_str and
+    lsqpack_qhuff_enc_str_size == qenc_enc_str_size (oracle) for prefixes
+    3/5/7, both dst[0] states and dst_len around the need (-1 included)."""
+    files = [os.path.join(DATA, f + ".qif") for f in ("netbsd", "fb-req",
+                                                      "fb-resp")]
+    r = subprocess.run([HOOK_TEST, "enc"] + files, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout and "misses 0" in r.stdout
+
+
+@pytest.mark.gpu
+def test_hook_decoder_seam_matches_lsqpack_huff_decode():
+    """Every Huffman literal of the reference's interop streams through one
+    memo batch per file: the patched lsqpack_huff_decode (lookup, else the
+    reference decoder) == lsqpack_huff_decode (oracle) in status, n_dst,
+    n_src and bytes for dst_len around the decoded length."""
+    files = [os.path.join(DATA, f + ".out.256.100.1")
+             for f in ("netbsd", "fb-req", "fb-resp")]
+    r = subprocess.run([HOOK_TEST, "dec"] + files, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
