@@ -13,7 +13,15 @@ collective on the data path: "scaling": "weak").
 
 Input buffers are rotated over --copies device copies (default 4, > 512 MB
 footprint) so a step does not re-read the previous step's bytes from the
-256 MB Infinity Cache.
+256 MB Infinity Cache.  Ranks meet only at the timing barrier and the
+max-over-ranks of the wall time, both over gloo on the host: no RCCL.
+
+--config4: ONE process, one host thread + HIP
+stream + qhuff context per GPU; a 16M-string batch is split by
+qhuff_shard_cuts into G byte-balanced contiguous shards, each GPU encodes
+and decodes its shard per step, and the shard outputs are stitched back
+(shard bases added on the host) and checked against a single-GPU pass over
+the whole batch.
 """
 import argparse
 import json
@@ -45,7 +53,14 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="wall seconds per CPU-baseline leg (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="CPU baseline threads (0 = all usable cores, <= 16)")
+                    help="CPU baseline 'all' leg threads (0 = every CPU this "
+                         "process may use: affinity, capped by the cgroup "
+                         "CPU quota)")
+    ap.add_argument("--config4", action="store_true",
+                    help="one process, G = --gpus devices, 16M strings split "
+                         "by qhuff_shard_cuts (no RCCL)")
+    ap.add_argument("--n4", type=int, default=16 << 20,
+                    help="--config4 total strings (default 16M)")
     ap.add_argument("--host-path", action=argparse.BooleanOptionalAction,
                     default=True,
                     help="also time the PCIe-inclusive host-memory path "
@@ -68,12 +83,43 @@ def cpu_model():
     return None
 
 
-def usable_cores():
+def host_cpus():
+    """What the CPU baseline can use: logical CPUs in the affinity mask,
+    capped by the cgroup CPU quota (a GPU box shares its host), plus the
+    machine's sockets / physical cores / SMT from /proc/cpuinfo."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(n, 16))
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    sockets, cores, logical = set(), set(), 0
+    phys = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "processor":
+                    logical += 1
+                elif k == "physical id":
+                    phys = v
+                    sockets.add(v)
+                elif k == "core id":
+                    cores.add((phys, v))
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"usable": usable, "affinity": aff,
+            "cgroup_quota_cpus": quota, "nproc": os.cpu_count(),
+            "sockets": len(sockets) or None,
+            "physical_cores": len(cores) or None,
+            "smt": (logical // len(cores)) if cores else None}
 
 
 def main():
@@ -86,8 +132,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config4:
+        return run_config4(args, np, torch, qhuff)
     if world > 1:
-        dist.init_process_group("nccl")
+        # timing barrier + max-over-ranks only: host-side gloo, no RCCL
+        dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -164,6 +213,7 @@ def main():
            if i % ev_every == ev_every - 1 else None
            for i in range(args.steps)]
     ev_used = [e for e in evs if e]
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -177,14 +227,17 @@ def main():
     wall = t1 - t0
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev_used) / len(ev_used)
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev_used) / len(ev_used)
+    # the kernels' sticky error word (look-back spin / offset range): a
+    # launch that raised one produced no valid output
+    dev_err = codec.device_error()
 
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall, 0.0 if ok_dec else 1.0, float(dev_err)],
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-        okt = torch.tensor([1.0 if ok_dec else 0.0], device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok_dec = bool(okt.item() > 0.5)
+        wall = float(t[0])
+        ok_dec = bool(t[1] < 0.5)
+        dev_err = int(t[2])
 
     ms_per_step = wall * 1e3 / args.steps
     bytes_per_step = 2 * raw_bytes           # raw in (encode) + raw out (decode)
@@ -221,30 +274,7 @@ def main():
     # ---- CPU baseline (rank 0, N = 1 only) -------------------------------------
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_lib
-        threads = args.cpu_threads or usable_cores()
-
-        def leg(buf, offs, op, payload_bytes):
-            best, tot, reps = 1e30, 0.0, 0
-            while tot < args.cpu_seconds or reps < 2:
-                dt = oracle_lib.bench_pass(buf, offs, op, threads)
-                best = min(best, dt)
-                tot += dt
-                reps += 1
-            return payload_bytes / best / 1e9, reps
-
-        enc_gbs, r1 = leg(data, off, 0, raw_bytes)
-        dec_gbs, r2 = leg(h_np, h_off_np, 1, raw_bytes)
-        both = 2.0 / (1.0 / enc_gbs + 1.0 / dec_gbs)
-        cpu = {"value": round(both, 3), "unit": "GB/s", "cores": threads,
-               "kind": "port",
-               "sample": ("full %d-string batch, oracle restatement of "
-                          "lsqpack_enc_enc_str(7,..) + lsqpack_huff_decode "
-                          "(fast path), best of %d/%d passes, %d threads"
-                          % (n, r1, r2, threads)),
-               "enc_gbps": round(enc_gbs, 3), "dec_gbps": round(dec_gbs, 3),
-               "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
+        cpu = cpu_baseline(args, data, off, h_np, h_off_np, n, raw_bytes)
 
     # ---- header hashing, outside the timed step --------
     # the batch read as n/2 (name, value) headers: XXH32 name + name/value
@@ -329,6 +359,7 @@ def main():
             "enc_payload_gbps": round(raw_bytes / (enc_ms * 1e-3) / 1e9, 2),
             "dec_payload_gbps": round(raw_bytes / (dec_ms * 1e-3) / 1e9, 2),
             "roundtrip_ok": bool(ok_dec),
+            "device_error": dev_err,
             "xxh32_headers": hashing,
             "roofline": roof, "cpu_baseline": cpu,
         }
@@ -338,6 +369,188 @@ def main():
     codec.close()
     if world > 1:
         dist.destroy_process_group()
+    if dev_err or not ok_dec:
+        sys.exit("bench: device error %d / round trip %s: the line above is "
+                 "not a valid measurement" % (dev_err, ok_dec))
+
+
+def cpu_baseline(args, data, off, h_np, h_off_np, n, raw_bytes):
+    """The oracle (a restatement of lsqpack_enc_enc_str(7, ..) and
+    lsqpack_huff_decode's fast path) over the same batch: one thread, then
+    every CPU this process may use.  `value` is the all-CPU
+    leg."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    cpus = host_cpus()
+    t_all = args.cpu_threads or cpus["usable"]
+
+    def leg(buf, offs, op, threads):
+        best, tot, reps = 1e30, 0.0, 0
+        while tot < args.cpu_seconds or reps < 2:
+            dt = oracle_lib.bench_pass(buf, offs, op, threads)
+            best = min(best, dt)
+            tot += dt
+            reps += 1
+        return raw_bytes / best / 1e9, reps
+
+    legs = {}
+    for name, threads in (("threads_1", 1), ("threads_all", t_all)):
+        e, r1 = leg(data, off, 0, threads)
+        d, r2 = leg(h_np, h_off_np, 1, threads)
+        legs[name] = {"threads": threads, "enc_gbps": round(e, 3),
+                      "dec_gbps": round(d, 3),
+                      "gbps": round(2.0 / (1.0 / e + 1.0 / d), 3),
+                      "passes": [r1, r2]}
+    return {"value": legs["threads_all"]["gbps"], "unit": "GB/s",
+            "cores": t_all, "kind": "port",
+            "sample": ("full %d-string batch, oracle restatement of "
+                       "lsqpack_enc_enc_str(7,..) + lsqpack_huff_decode (fast "
+                       "path), best pass of >= %.0f s per leg, at 1 thread and "
+                       "at every usable CPU" % (n, args.cpu_seconds)),
+            "threads_1": legs["threads_1"], "threads_all": legs["threads_all"],
+            "host": cpus, "cpu_model": cpu_model()}
+
+
+def run_config4(args, np, torch, qhuff):
+    """Config 4: one batch of --n4 strings over G GPUs of one process."""
+    import threading
+    G = args.gpus
+    if torch.cuda.device_count() < G:
+        sys.exit("config4: %d GPUs requested, %d visible"
+                 % (G, torch.cuda.device_count()))
+    alpha = (qhuff.TOKEN_ALPHABET if args.alphabet == "token"
+             else qhuff.BASE64_ALPHABET)
+    N = args.n4
+    data, off = qhuff.synth_batch(N, seed=0x9E3779B97F4A7C15, alphabet=alpha)
+    cuts = qhuff.shard_cuts(off, G)
+    from qhuff import shard as S
+    copies = max(1, min(args.copies, 2))
+    barrier = threading.Barrier(G)
+    res = [None] * G
+    errs = []
+
+    def worker(g):
+        try:
+            torch.cuda.set_device(g)
+            dev = torch.device("cuda", g)
+            sd, soff, _ = S.shard_view(data, off, cuts, g)
+            n = len(soff) - 1
+            raw = int(soff[-1])
+            codec = qhuff.Codec(g)
+            st = torch.cuda.Stream(device=dev)
+            with torch.cuda.stream(st):
+                d_in = [torch.from_numpy(np.ascontiguousarray(sd)).to(dev)
+                        for _ in range(copies)]
+                d_off = [torch.from_numpy(soff.view(np.int32)).to(dev)
+                         for _ in range(copies)]
+                ecap = qhuff.encode_bound(raw, n, 0)
+                e_out = [torch.empty(ecap, dtype=torch.uint8, device=dev)
+                         for _ in range(copies)]
+                e_off = [torch.empty(n + 1, dtype=torch.int32, device=dev)
+                         for _ in range(copies)]
+                # decode input: this shard's Huffman payloads, made once
+                codec.encode_into(d_in[0], d_off[0], n, 0, e_out[0], e_off[0],
+                                  st)
+                st.synchronize()
+                hb = int(e_off[0][-1].item())
+                h_in = [e_out[0][:hb].clone() for _ in range(copies)]
+                h_off = [e_off[0].clone() for _ in range(copies)]
+                dcap = qhuff.decode_bound(hb, n)
+                o_out = [torch.empty(dcap, dtype=torch.uint8, device=dev)
+                         for _ in range(copies)]
+                o_off = [torch.empty(n + 1, dtype=torch.int32, device=dev)
+                         for _ in range(copies)]
+                o_st = [torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+                        for _ in range(copies)]
+            st.synchronize()
+
+            def step(i):
+                k = i % copies
+                codec.encode_into(d_in[k], d_off[k], n, 0, e_out[k], e_off[k],
+                                  st)
+                codec.decode_into(h_in[k], h_off[k], n, o_out[k], o_off[k],
+                                  o_st[k], st)
+
+            for i in range(args.warmup):
+                step(i)
+            st.synchronize()
+            barrier.wait()
+            st.synchronize()
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                step(args.warmup + i)
+            st.synchronize()
+            t1 = time.perf_counter()
+            barrier.wait()
+            k = (args.warmup + args.steps - 1) % copies
+            eo = e_off[k].cpu().numpy().view(np.uint32).copy()
+            res[g] = {"wall": t1 - t0, "n": n, "raw": raw, "huff": hb,
+                      "enc": (e_out[k][:int(eo[-1])].cpu().numpy(), eo),
+                      "dec": (o_out[k][:raw].cpu().numpy(),
+                              o_off[k].cpu().numpy().view(np.uint32).copy()),
+                      "status_ok": bool((o_st[k][:n] == 0).all().item()),
+                      "device_error": codec.device_error()}
+            codec.close()
+        except BaseException as e:          # surface in the main thread
+            errs.append((g, repr(e)))
+            barrier.abort()
+
+    ths = [threading.Thread(target=worker, args=(g,)) for g in range(G)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    if errs:
+        sys.exit("config4 worker failed: %r" % errs)
+
+    wall = max(r["wall"] for r in res)
+    raw_total = int(off[-1])
+    value = 2 * raw_total * args.steps / wall / 1e9
+
+    # stitched output == one pass over the whole batch on GPU 0
+    enc_m, enc_moff = S.merge([r["enc"] for r in res])
+    dec_m, dec_moff = S.merge([r["dec"] for r in res])
+    torch.cuda.set_device(0)
+    c0 = qhuff.Codec(0)
+    d_all = torch.from_numpy(data).cuda(0)
+    o_all = torch.from_numpy(off.view(np.int32)).cuda(0)
+    ref_out, ref_off = c0.encode(d_all, o_all, 0)
+    torch.cuda.synchronize()
+    ref_off = ref_off.cpu().numpy().view(np.uint32)
+    stitched_ok = (np.array_equal(enc_moff, ref_off) and np.array_equal(
+        enc_m, ref_out[:int(ref_off[-1])].cpu().numpy()))
+    roundtrip_ok = (np.array_equal(dec_moff, off)
+                    and np.array_equal(dec_m, data)
+                    and all(r["status_ok"] for r in res))
+    c0.close()
+    dev_err = max(r["device_error"] for r in res)
+    shard_bytes = [r["raw"] for r in res]
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GB/s",
+        "n_gpus": G, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall * 1e3 / args.steps, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (xorshift64 %s alphabet, U[8,64] B strings)"
+                % args.alphabet,
+        "config": {"workload": "config4", "strings": N,
+                   "raw_bytes": raw_total,
+                   "parallelism": "%d GPUs, one host thread + stream + "
+                                  "qhuff_ctx each, qhuff_shard_cuts "
+                                  "byte-balanced shards, no collective" % G,
+                   "shard_strings": [r["n"] for r in res],
+                   "shard_raw_bytes": shard_bytes,
+                   "shard_byte_balance": round(max(shard_bytes)
+                                               / max(1, min(shard_bytes)), 6)},
+        "per_gpu": [{"gpu": g, "wall_ms": round(r["wall"] * 1e3, 3),
+                     "gbps": round(2 * r["raw"] * args.steps / r["wall"]
+                                   / 1e9, 3)} for g, r in enumerate(res)],
+        "stitched_equals_single_pass": bool(stitched_ok),
+        "roundtrip_ok": bool(roundtrip_ok), "device_error": dev_err,
+    }
+    print(json.dumps(line), flush=True)
+    if dev_err or not stitched_ok or not roundtrip_ok:
+        sys.exit("config4: check failed")
 
 
 if __name__ == "__main__":
