@@ -577,6 +577,7 @@ struct DecPolicy
     {
         ch.store<true>((QH_LDS u32x4 *) wv->in, sp.n16);
     }
+    __device__ __forceinline__ void prepare(const Span &) {}
     __device__ __forceinline__ const QH_LDS uint32_t *out_stage() const
     {
         return wv->in;

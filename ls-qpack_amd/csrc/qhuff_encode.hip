@@ -458,8 +458,7 @@ dense_or(QH_LDS uint32_t *dense, uint32_t pos, uint32_t v, uint32_t len)
 // codes shift every offset by the same amount).  Returns whether the dense
 // stream is usable: every code of the span at most 15 bits.
 __device__ __forceinline__ bool
-dense_pass(const Chunks<kChunks> &ch, uint32_t n16, const QH_LDS uint32_t *mt,
-           QH_LDS EncWave *wv)
+dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
 {
     const uint32_t lane = lane_id();
     QH_LDS u32x4 *d4 = (QH_LDS u32x4 *) wv->dense;
@@ -472,10 +471,11 @@ dense_pass(const Chunks<kChunks> &ch, uint32_t n16, const QH_LDS uint32_t *mt,
     for (int k = 0; k < kChunks; ++k)
     {
         // every row is coded (no exit for short spans): straight-line code
-        // lets the rows' lookups overlap; chunks past the span are clamped
-        // copies of its last chunk, coded past its end and never read
+        // lets the rows' lookups overlap; chunks past the span read its last
+        // staged chunk again, coded past its end and never read
         const uint32_t c = lane + 64u * k;
-        const u32x4 w = ch.ch[k];
+        const uint32_t last = n16 ? n16 - 1 : 0;
+        const u32x4 w = ((const QH_LDS u32x4 *) wv->in)[c < last ? c : last];
         const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
         uint32_t m[16];
 #pragma unroll
@@ -682,12 +682,17 @@ struct EncPolicy
     EncSize z;
     bool dense;                      // wave-uniform: tile from the dense stream
 
-    // staged tile: chunks into the LDS stage, the byte-parallel pass
+    // staged tile: chunks into the LDS stage
     __device__ __forceinline__ void stage_in(const Chunks<kChunks> &ch,
                                              const Span &sp, const TileOffs &)
     {
         ch.store<false>((QH_LDS u32x4 *) wv->in, sp.n16);
-        dense = dense_pass(ch, sp.n16, sm->mt, wv);
+    }
+    // the byte-parallel pass over the stage (after the next tile's loads
+    // have been issued into the chunk registers)
+    __device__ __forceinline__ void prepare(const Span &sp)
+    {
+        dense = dense_pass(sp.n16, sm->mt, wv);
     }
     __device__ __forceinline__ const QH_LDS uint32_t *out_stage() const
     {

@@ -7,31 +7,31 @@
 // look-back waits on belongs to a running wave, whatever the residency.
 // Per iteration, for tile t:
 //
-//   top    one wait for everything the last iteration issued, a whole codec
-//          ago: t's input chunks and offsets, the older pending tile's
-//          look-back polls, the newer one's super-accumulator add, the
-//          stores of the tile before.  Publish the newer tile's super
-//          aggregate if its add completed the super tile; resolve the older
-//          pending tile's look-back and store its output (registers).
-//          P::stage_in() -- t's chunks into the LDS stage (the encoder also
-//          runs its byte-parallel pass here, on the chunk registers) -- then
-//          issue the loads of the next tile's input and of the offsets of
-//          the tile after it (and the next ticket), so they have the whole
-//          codec to land
-//   codec  P::codec() -- LDS only -- per-lane output size (+ status)
+//   top    one wait for what the last iteration issued: t's input chunks and
+//          offsets and the ticket (a whole codec ago), the stores and the
+//          look-back start of the last iteration (an emit ago).  Publish the
+//          newer tile's super aggregate if its add completed the super tile.
+//          P::stage_in()
+//          -- t's chunks into the LDS stage -- then the loads of the next
+//          tile's input, of the offsets of the tile after it and the next
+//          ticket, and the older pending tile's look-back polls: all of them
+//          have the whole codec to land
+//   codec  P::prepare() (the encoder's byte-parallel pass over the stage),
+//          P::codec() -- LDS only -- per-lane output size (+ status)
+//   flush  one wait (the polls); resolve the older pending tile's look-back
+//          and store its output (registers)
 //   scan   wave scan -> tile-local offsets, tile total; publish the tile
 //          aggregate and add it to the super accumulator (LookBack::start)
 //   emit   P::emit() -- compacted output of t into the LDS out stage --
 //          gathered into registers (TileOut)
-//   poll   issue the older pending tile's look-back polls
 //
 // Two tiles are pending at a time, both holding their output in registers:
-// tile k's look-back is resolved at the top of iteration k + 2, its windows
-// polled at the end of iteration k + 1, a whole codec after every tile
-// before it published its aggregate.
+// tile k's look-back windows are polled at the top of iteration k + 2, a
+// whole iteration after every tile before it published its aggregate, and
+// resolved after that iteration's codec.
 //
 // Tiles whose input or output does not fit the stages are coded eagerly by
-// P::slow_tile() (out of line) after the pending tile has been flushed.
+// P::slow_tile() (out of line) after the pending tiles have been flushed.
 #pragma once
 
 #include "qhuff_kernels.h"
@@ -155,30 +155,29 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     for (;; ++it)
     {
         prof_stamp(c, it, 0);
-        // top: one wait for everything the last iteration issued -- the
-        // input of t, offsets, the held tile's polls, the newer tile's
-        // super-accumulator add, the stores of the tile before, the ticket
+        // top: t's input, offsets and ticket (issued a codec ago), the last
+        // iteration's stores and look-back start (an emit ago)
         wait_vm_all();
         prof_stamp(c, it, 1);
+        // the newer tile's add has returned: publish the super aggregate if
+        // it completed its super tile (as early as possible: look-backs of
+        // later super tiles wait on it)
         if (newer.valid)
             newer.lb.super_agg(c);
-        if (older.valid)
-            flush_tile<P::kStatus>(c, older, older_out, out, out_off, status,
-                                   n, it);
-        older = newer;
-        older_out = newer_out;
-        newer.valid = false;
         if (sp_cur.staged)
             pol.stage_in(ch, sp_cur, o_cur);
         wave_sync();
         // loads for the next tiles, a whole codec ahead of their use: input
-        // of tn, offsets of the ticketed tile after it, the next ticket
+        // of tn, offsets of the ticketed tile after it, the next ticket; the
+        // older pending tile's look-back polls
         const uint32_t tnn = tn < nt ? tk.tile_of(kq) : kNone;
         const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), kStageCap);
         ch.load(sp_nxt);
         const uint32_t tz = clamp(tnn);
         o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
         kq = tnn < nt ? tk.claim(c) : kNone;
+        if (older.valid)
+            older.lb.poll(c);
         prof_stamp(c, it, 2);
 
         // codec of t (LDS only when staged)
@@ -186,12 +185,26 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         uint32_t sz = 0, st = 0;
         bool fast = sp_cur.staged;
         if (fast)
+        {
+            pol.prepare(sp_cur);
             pol.codec(o_cur, cnt, sp_cur, &sz, &st);
+        }
         const uint32_t incl = wave_incl_scan(sz);
         const uint32_t excl = incl - sz;
         const uint32_t total = read_lane(incl, 63);
         fast = fast && total + 64 <= (uint32_t) kStageCap;
         prof_stamp(c, it, 3);
+
+        // the polls (a codec ago); resolve + store the older tile
+        wait_vm_all();
+        prof_stamp(c, it, 4);
+        if (older.valid)
+            flush_tile<P::kStatus>(c, older, older_out, out, out_off, status,
+                                   n, it);
+        older = newer;
+        older_out = newer_out;
+        newer.valid = false;
+        prof_stamp(c, it, 5);
 
         if (fast)
         {
@@ -202,7 +215,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
             newer.excl = excl;
             newer.stat = st;
             newer.lb.start(c, t, total);
-            prof_stamp(c, it, 4);
             wave_sync();
             pol.emit(excl, sz, total);
             wave_sync();
@@ -219,9 +231,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
             pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
                           status, n);
         }
-        if (older.valid)
-            older.lb.poll(c);
-        prof_stamp(c, it, 5);
         wave_sync();
         prof_stamp(c, it, 6);
 
@@ -237,7 +246,10 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     if (newer.valid)
         newer.lb.super_agg(c);
     if (older.valid)
+    {
+        older.lb.poll(c);
         flush_tile<P::kStatus>(c, older, older_out, out, out_off, status, n);
+    }
     if (newer.valid)
     {
         newer.lb.poll(c);

@@ -44,8 +44,9 @@ mb_encode(EncArgs a, int reps, MbOut *res)
     for (int r = 0; r < reps; ++r)
     {
         const uint64_t t0 = __builtin_amdgcn_s_memtime();
-        pol.stage_in(ch, sp, to);            // dense pass included
+        pol.stage_in(ch, sp, to);
         wave_sync();
+        pol.prepare(sp);                     // the encoder's dense pass
         uint32_t sz, st;
         pol.codec(to, kWT, sp, &sz, &st);
         const uint32_t incl = wave_incl_scan(sz);

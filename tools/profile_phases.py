@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Per-phase cycle breakdown of the wave pipeline from a QHUFF_PROFILE build
 (make -C ls-qpack_amd prof; run with QHUFF_LIB=.../libqhuff_prof.so).
-Slots per wave iteration (qhuff_pipeline.h): 0 top, 1 after the drain,
-2 after stage + loads + polls, 3 after codec + scan, 4 after lb.start,
-5 after the deferred flush, 6 end of iteration."""
+Slots per wave iteration (qhuff_pipeline.h): 0 top, 1 after the top wait,
+2 after stage + loads + polls, 3 after codec + scan, 4 after the poll wait,
+7 after the older tile's look-back (inside the flush), 5 after the flush,
+9 after lb.start + emit, 6 end of iteration (after the gather)."""
 import os
 import sys
 
@@ -17,8 +18,8 @@ import torch
 import qhuff
 
 ITERS, SLOTS = 16, 12
-NAMES = ["drain", "flush+park+stage", "codec+scan", "loads+lb.start",
-         "emit+gather+poll", "end"]
+NAMES = ["top wait", "stage+loads+polls", "codec+scan", "poll wait",
+         "flush", "start+emit+gather"]
 
 
 def report(tag, p):
@@ -36,19 +37,19 @@ def report(tag, p):
             print("  %-12s mean %8.0f  p50 %8.0f  p90 %8.0f  max %8.0f cyc"
                   % (NAMES[ph], d.mean(), np.median(d), np.percentile(d, 90),
                      d.max()))
-    ok = live & (p[:, :, 1] != 0) & (p[:, :, 7] != 0)
+    ok = live & (p[:, :, 4] != 0) & (p[:, :, 7] != 0)
     if ok.any():
-        lbt = (p[:, :, 7] - p[:, :, 1])[ok]
-        stt = (p[:, :, 2] - p[:, :, 7])[ok]
+        lbt = (p[:, :, 7] - p[:, :, 4])[ok]
+        stt = (p[:, :, 5] - p[:, :, 7])[ok]
         sp = p[:, :, 8][ok]
-        print("  flush: look-back mean %.0f p90 %.0f | stores+park+stage mean %.0f | re-polls mean %.2f, >0 in %.1f%%, max %d"
+        print("  flush: look-back mean %.0f p90 %.0f | stores mean %.0f | re-polls mean %.2f, >0 in %.1f%%, max %d"
               % (lbt.mean(), np.percentile(lbt, 90), stt.mean(), sp.mean(),
                  100.0 * (sp > 0).mean(), sp.max()))
-    ok = live & (p[:, :, 4] != 0) & (p[:, :, 9] != 0)
+    ok = live & (p[:, :, 5] != 0) & (p[:, :, 9] != 0)
     if ok.any():
-        a = (p[:, :, 9] - p[:, :, 4])[ok]
-        b = (p[:, :, 5] - p[:, :, 9])[ok]
-        print("  emit: emit mean %.0f p90 %.0f | gather+poll mean %.0f p90 %.0f"
+        a = (p[:, :, 9] - p[:, :, 5])[ok]
+        b = (p[:, :, 6] - p[:, :, 9])[ok]
+        print("  start+emit mean %.0f p90 %.0f | gather mean %.0f p90 %.0f"
               % (a.mean(), np.percentile(a, 90), b.mean(), np.percentile(b, 90)))
     if not os.environ.get("TIMELINE"):
         return
