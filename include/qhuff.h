@@ -272,7 +272,8 @@ int qhuff_xxh32_headers_host(qhuff_ctx *ctx, const uint8_t *in,
                              const uint32_t *off, uint32_t n, uint32_t seed,
                              uint32_t *name_hash, uint32_t *nameval_hash);
 
-/* Last HIP error string for this context (diagnostics). */
+/* Last HIP error string for this context (diagnostics); with ctx == NULL,
+ * the reason of the calling thread's last failed qhuff_open. */
 const char *qhuff_last_error(qhuff_ctx *ctx);
 
 /* Synchronise the device and return (then clear) the context's sticky device

@@ -26,20 +26,13 @@
 // tile's output base.
 #include "qhuff_pipeline.h"
 
-// 1: decoded bytes go to the arena as one unaligned 2-byte store per step
-// instead of two byte stores -- measured 45% slower on MI355X (unaligned LDS
-// stores are split), kept off
-#ifndef QH_EMIT_B16
-#define QH_EMIT_B16 0
-#endif
-
-// 1: held lanes of the LDS main loop read a hold entry (see
-// decode_string_lds); 0: per-lane gating selects
-#ifndef QH_HOLD_ENTRY
-#define QH_HOLD_ENTRY 1
-#endif
-
 namespace qhuff {
+
+// window entry fields (qhuff_tables.h)
+__device__ __forceinline__ uint32_t ent_c(uint32_t e) { return (e >> 8) & 15; }
+__device__ __forceinline__ uint32_t ent_l0(uint32_t e) { return (e >> 12) & 15; }
+__device__ __forceinline__ uint32_t ent_ns(uint32_t e) { return (e >> 24) & 3; }
+__device__ __forceinline__ uint32_t ent_sym1(uint32_t e) { return (e >> 16) & 0xff; }
 
 constexpr int kDecInCap = kStageCap;                   // staged input bytes
 // byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
@@ -62,7 +55,7 @@ struct DecSmem
     uint32_t win[kWinSize + 4];      // + the hold entry
     uint16_t sorted[257];
     DecWave w[kWaves];
-    uint32_t tk[2];                  // the block's first two tickets
+    BlockTickets tk;                 // the workgroup's first tickets
 };
 
 struct DecLds                        // big-endian dwords staged in LDS
@@ -136,7 +129,7 @@ main_step(bool act, uint32_t d, uint32_t &hi, uint32_t &lo, uint32_t &bits,
         const uint32_t sym = long_code(hi, s_sorted, &L);
         const bool lng = (GATED ? act : true) & (e < (1u << 24));
         ok = !(lng & (sym == 256));
-        const uint32_t el = (sym & 0xff) | (L << 16) | (1u << 24)
+        const uint32_t el = (sym & 0xff) | (L << 8) | (L << 12) | (1u << 24)
                           | ((32u - L) << 26);
         e = lng ? (ok ? el : 0u) : e;
     }
@@ -216,8 +209,7 @@ decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
     {
         const uint32_t w = hi | (0xffffffffu >> (rem & 31));
         const uint32_t e = s_win[w >> (32 - kWinBits)];
-        const uint32_t ns = (e >> 24) & 3, ct = (e >> 16) & 15,
-                       l0 = (e >> 20) & 15;
+        const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
         const bool two = (ns == 2) & (ct <= rem);
         uint32_t c = two ? ct : (ns ? l0 : 31u);
         uint32_t val = e;
@@ -252,10 +244,13 @@ decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
 
 // Lean variant used by the staged (LDS) path.  The bit buffer is one 64-bit
 // register, MSB = next bit, holding >= 32 valid bits at every main step; the
-// dword that refills it is read one step ahead (`nx`), so only the window
-// lookup sits on the step's dependency chain.  Main steps run while a lane
-// has >= 32 real bits left (lanes past that are masked off); the EOS check
-// lives in the rare long-code branch.  The last < 32 bits take the padded
+// dword that refills it is read beside the table lookup, so only the lookup
+// sits on the step's dependency chain.  Main steps run while a lane has at
+// least kWinBits real bits left, so the window holds no padding and every
+// symbol of its entry is real (a lane past that reads the hold entry: it
+// consumes and emits nothing); the EOS check and the "code runs past the
+// end" check (the leftover would be >= 8 bits: D3) live in the rare long-code
+// branch.  The last < kWinBits bits (at most two symbols) take the padded
 // epilogue with the D3 tail rule, exactly as decode_string().
 template <class Emit>
 __device__ __forceinline__ int
@@ -275,38 +270,37 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         nx = src[p];
     }
     uint32_t bad = 0;                        // (a u32: no lane-mask phis)
-    // one loop, no lane branches: a lane with < 32 real bits left steps with
-    // c = ns = 0 (its two arena byte writes land at its current end and are
-    // overwritten by the epilogue); the long-code fix is computed for the
-    // whole wave with selects, behind a wave-uniform branch.  The next
-    // window is taken from the shifted buffer BEFORE the refill: a step of
-    // <= 12 bits leaves >= 20 valid bits, so the step's dependency chain is
-    // lookup -> length -> shift -> index, with the refill beside it (after a
-    // long code the index is recomputed behind a second uniform branch)
-#if QH_HOLD_ENTRY
-    // a lane with < 32 real bits left looks up the hold entry instead of
-    // its window (c = ns = 0, never a long code), so the step needs no
-    // per-lane gating and the long-code ballot no lane mask
-    uint32_t idx = rem >= 32 ? (uint32_t) (buf >> (64 - kWinBits)) : kHoldIdx;
-    if (__builtin_amdgcn_ballot_w64(rem >= 32))
+    // One loop, no lane branches: a lane with < kWinBits real bits left
+    // looks up the hold entry (c = ns = 0, never a long code); its two arena
+    // byte writes land at its current end and are overwritten by the
+    // epilogue.  The long-code fix is computed for the whole wave with
+    // selects, behind a wave-uniform branch.  The next window is taken from
+    // the shifted buffer BEFORE the refill: a step of <= 13 bits leaves >= 19
+    // valid bits, so the step's dependency chain is lookup -> length ->
+    // shift -> index, with the refill beside it (after a long code the index
+    // is recomputed behind a second uniform branch).
+    constexpr uint32_t kMain = kWinBits;
+    uint32_t idx = rem >= kMain ? (uint32_t) (buf >> (64 - kWinBits)) : kHoldIdx;
+    if (__builtin_amdgcn_ballot_w64(rem >= kMain))
     do
     {
         uint32_t e = s_win[idx];
-        uint32_t c = (e >> 16) & 15;          // bits of the entry's symbols
-        uint32_t ns = (e >> 24) & 3;          // symbols (0: longer code)
+        uint32_t c = ent_c(e);                // bits of the entry's symbols
+        uint32_t ns = ent_ns(e);              // symbols (0: longer code)
         const bool any_long = __builtin_amdgcn_ballot_w64(e < (1u << 24)) != 0;
         if (any_long)
         {
-            // a code of 14..30 bits (EOS rejects the string, D3 (a))
+            // a code of 14..30 bits; EOS, or a code running past the end,
+            // rejects the string (D3)
             const bool lng = e < (1u << 24);
             uint32_t L;
             const uint32_t sym = long_code((uint32_t) (buf >> 32), s_sorted, &L);
-            const bool eos = lng & (sym == 256);
+            const bool rej = lng & ((sym == 256) | (L > rem));
             e = lng ? sym : e;
-            c = lng ? (eos ? 0u : L) : c;
-            ns = lng ? (eos ? 0u : 1u) : ns;
-            bad |= eos ? 1u : 0u;
-            rem = eos ? 0u : rem;
+            c = lng ? (rej ? 0u : L) : c;
+            ns = lng ? (rej ? 0u : 1u) : ns;
+            bad |= rej ? 1u : 0u;
+            rem = rej ? 0u : rem;
         }
         buf <<= c;
         idx = (uint32_t) (buf >> (64 - kWinBits));
@@ -321,51 +315,10 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         nx = src[p];
         if (any_long)
             idx = (uint32_t) (buf >> (64 - kWinBits));
-        idx = rem >= 32 ? idx : kHoldIdx;
-    } while (__builtin_amdgcn_ballot_w64(rem >= 32));
-#else
-    uint32_t idx = (uint32_t) (buf >> (64 - kWinBits));
-    if (__builtin_amdgcn_ballot_w64(rem >= 32))
-    do
-    {
-        const bool act = rem >= 32;
-        uint32_t e = s_win[idx];
-        uint32_t c = (e >> 16) & 15;          // bits of the entry's symbols
-        uint32_t ns = (e >> 24) & 3;          // symbols (0: longer code)
-        const bool lng = act & (e < (1u << 24));
-        const bool any_long = __builtin_amdgcn_ballot_w64(lng) != 0;
-        if (any_long)
-        {
-            // a code of 13..30 bits (EOS rejects the string, D3 (a))
-            uint32_t L;
-            const uint32_t sym = long_code((uint32_t) (buf >> 32), s_sorted, &L);
-            const bool eos = lng & (sym == 256);
-            e = lng ? sym : e;
-            c = lng ? (eos ? 0u : L) : c;
-            ns = lng ? (eos ? 0u : 1u) : ns;
-            bad |= eos ? 1u : 0u;
-            rem = eos ? 0u : rem;
-        }
-        c = act ? c : 0u;
-        ns = act ? ns : 0u;
-        buf <<= c;
-        idx = (uint32_t) (buf >> (64 - kWinBits));
-        emit(e, ns);
-        bits -= c;
-        rem -= c;
-        const bool need = bits < 32;
-        const uint32_t dd = need ? nx : 0u;
-        buf |= (uint64_t) dd << ((32 - bits) & 31);
-        bits += need ? 32u : 0u;
-        p += need ? 1u : 0u;
-        nx = src[p];
-        if (any_long)
-            idx = (uint32_t) (buf >> (64 - kWinBits));
-    } while (__builtin_amdgcn_ballot_w64(rem >= 32));
+        idx = rem >= kMain ? idx : kHoldIdx;
+    } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
 
-#endif
-
-    // epilogue: the last < 32 bits, padded with ones; D3 tail rule
+    // epilogue: the last < kWinBits bits, padded with ones; D3 tail rule
     bool fin = bad || rem == 0;
     if (__builtin_amdgcn_ballot_w64(!fin))
     do
@@ -373,8 +326,7 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         const uint32_t hi = (uint32_t) (buf >> 32);
         const uint32_t w = hi | (0xffffffffu >> (rem & 31));
         const uint32_t e = s_win[w >> (32 - kWinBits)];
-        const uint32_t ns = (e >> 24) & 3, ct = (e >> 16) & 15,
-                       l0 = (e >> 20) & 15;
+        const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
         const bool two = (ns == 2) & (ct <= rem);
         uint32_t c = two ? ct : (ns ? l0 : 31u);
         uint32_t val = e;
@@ -406,57 +358,20 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
     return bad ? -1 : (int) emit.n;
 }
 
-// byte-granular arena sink: two unconditional byte stores per step (the
+// byte-granular arena sink: two unconditional byte stores per step, the
+// entry's first symbol [7:0] and second [23:16] (ds_write_b8 / _d16_hi; the
 // second is overwritten by the next step when only one symbol was emitted)
 struct ArenaEmit
 {
     QH_LDS uint8_t *slot;
+    QH_LDS uint8_t *p;
     uint32_t n;
-    __device__ __forceinline__ void finish() {}
+    __device__ __forceinline__ void finish() { n = (uint32_t) (p - slot); }
     __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
     {
-#if QH_EMIT_B16
-        // one 2-byte store at any byte address (LDS unaligned access)
-        *(QH_LDS uint16_t *) (slot + n) = (uint16_t) val;
-#else
-        slot[n] = (uint8_t) val;
-        slot[n + 1] = (uint8_t) (val >> 8);
-#endif
-        n += nb;
-    }
-};
-
-// arena sink accumulating bytes in registers: whole dwords go to a
-// dword-aligned arena slot as they fill (one LDS store per four output bytes
-// instead of two per step).  Measured slower than ArenaEmit on MI355X -- the
-// decode loop is issue/latency-bound, not LDS-bound -- kept for experiments;
-// finish() stores the partial last dword and sets n
-struct WordEmit
-{
-    QH_LDS uint32_t *slot;
-    uint32_t w;                      // dwords stored
-    uint32_t sh;                     // bits pending in acc: 0, 8, 16 or 24
-    uint64_t acc;
-    uint32_t n;                      // output bytes (after finish())
-    __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
-    {
-        // the entry's first nb symbol bytes (nb <= 2)
-        const uint32_t v = val & ((1u << (8 * nb)) - 1);
-        acc |= (uint64_t) v << sh;
-        sh += 8 * nb;
-        if (sh >= 32)
-        {
-            slot[w] = (uint32_t) acc;
-            acc >>= 32;
-            sh -= 32;
-            ++w;
-        }
-    }
-    __device__ __forceinline__ void finish()
-    {
-        if (sh)
-            slot[w] = (uint32_t) acc;
-        n = 4 * w + sh / 8;
+        p[0] = (uint8_t) val;
+        p[1] = (uint8_t) (val >> 16);
+        p += nb;
     }
 };
 
@@ -478,7 +393,7 @@ struct GlobalEmit                            // slow path: byte stores
         if (nb >= 1)
             dst[n] = (uint8_t) val;
         if (nb == 2)
-            dst[n + 1] = (uint8_t) (val >> 8);
+            dst[n + 1] = (uint8_t) (val >> 16);
         n += nb;
     }
 };
@@ -595,7 +510,7 @@ struct DecPolicy
         {
             const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
             const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
-            ArenaEmit em{wv->arena + slot0, 0};
+            ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
             r = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted,
                                   em);
         }
@@ -641,11 +556,12 @@ qhuff_decode_kernel(DecArgs a)
     }
     Tickets tk;
     tk.init();
-    claim_block_tickets(a.c, tk, sm->tk);
+    claim_block_tickets(a.c, tk, &sm->tk);
     __syncthreads();                 // the only workgroup barrier
     DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
-    const uint32_t w = (uint32_t) (tid >> 6);
-    tile_pipeline(pol, a.c, tk, sm->tk[0] + w, sm->tk[1] + w, a.in, a.in_off,
+    uint32_t k0, k1;
+    wave_tickets(tk, &sm->tk, &k0, &k1);
+    tile_pipeline(pol, a.c, tk, k0, k1, a.in, a.in_off,
                   a.n, a.out, a.out_off, a.status);
 }
 

@@ -152,6 +152,32 @@ wave_incl_scan(uint32_t v)
     return x;
 }
 
+// whole-wave DPP moves (gfx9 wavefront shifts): lane i gets lane i - 1's
+// value; lane 0 gets lane 63's (ror) or 0 (shr)
+__device__ __forceinline__ uint32_t
+wave_ror1(uint32_t v)
+{
+    return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x13c, 0xf, 0xf,
+                                                  false);
+}
+
+__device__ __forceinline__ uint32_t
+wave_shr1(uint32_t v)
+{
+    return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x138, 0xf, 0xf,
+                                                  false);
+}
+
+// sum over the wave of values below 2^40 (look-back flag values): two
+// 32-bit DPP scans of the low 16 and the high 24 bits, no LDS traffic
+__device__ __forceinline__ uint64_t
+wave_sum40(uint64_t v)
+{
+    const uint32_t lo = read_lane(wave_incl_scan((uint32_t) v & 0xffffu), 63);
+    const uint32_t hi = read_lane(wave_incl_scan((uint32_t) (v >> 16)), 63);
+    return ((uint64_t) hi << 16) + lo;
+}
+
 __device__ __forceinline__ uint32_t
 wave_max(uint32_t v)
 {
@@ -197,38 +223,44 @@ clear_next_launch(const Coord &c)
                            0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Tile tickets.  claim() issues the returning atomic (lane 0) and does not
-// wait for it; tile_of() reads the result (after a vmcnt wait).
+// Tile tickets.  Every wave belongs to one of kTickGroups ticket groups,
+// g = (blockIdx.x * kWaves + wave) % kTickGroups, so that the waves of ANY
+// single workgroup cover every group: tile k * kTickGroups + g is the k-th
+// ticket of group g, tickets of a group are handed out in order, and a
+// claimed tile is always held by a running wave.  A look-back only waits on
+// tiles with smaller indices, so whatever subset of the grid is resident
+// (another kernel, context or process on the GPU), the smallest unfinished
+// tile is held by a running wave or claimable by one.  (Groups tied to
+// workgroups, e.g. blockIdx % 8, follow the XCD the workgroup runs on: two
+// kernels that each miss one XCD could then wait on each other for ever.)
+// claim() issues the returning atomic (lane 0) and does not wait for it;
+// tile_of() reads the result (after a vmcnt wait).
+static_assert(kWaves >= (int) kTickGroups, "a workgroup must cover every ticket group");
+
 struct Tickets
 {
-    uint32_t g, G;                          // this block's group, group count
+    uint32_t g;                             // this wave's group
 
     __device__ __forceinline__ void init()
     {
-        G = gridDim.x < kTickGroups ? gridDim.x : kTickGroups;
-        g = blockIdx.x % G;
+        g = (blockIdx.x * (uint32_t) kWaves + (threadIdx.x >> 6)) % kTickGroups;
+    }
+    __device__ __forceinline__ uint32_t *counter(const Coord &c, uint32_t q) const
+    {
+        return &c.tick[((c.epoch & 1) * kTickGroups + q) * kTickStride];
     }
     __device__ __forceinline__ uint32_t claim(const Coord &c) const
     {
         uint32_t k = 0;
         if (lane_id() == 0)
-            k = __hip_atomic_fetch_add(
-                &c.tick[((c.epoch & 1) * kTickGroups + g) * kTickStride], 1u,
-                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            k = __hip_atomic_fetch_add(counter(c, g), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
         return k;
-    }
-    // claim m tickets at once (one thread; the caller hands them out)
-    __device__ __forceinline__ uint32_t claim_many(const Coord &c,
-                                                   uint32_t m) const
-    {
-        return __hip_atomic_fetch_add(
-            &c.tick[((c.epoch & 1) * kTickGroups + g) * kTickStride], m,
-            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // tile of ticket k (wave-uniform; ~0u past 2^32 tiles)
     __device__ __forceinline__ uint32_t tile_of_u(uint32_t k) const
     {
-        const uint64_t t = (uint64_t) k * G + g;
+        const uint64_t t = (uint64_t) k * kTickGroups + g;
         return t < 0xffffffffull ? (uint32_t) t : 0xffffffffu;
     }
     // tile of a ticket claim()ed by lane 0
@@ -506,8 +538,8 @@ struct LookBack
             const uint64_t upto = F >= 63 ? ~0ull : ((2ull << F) - 1);
             if ((inv & upto) == 0)
             {
-                excl = wave_sum((inq && (int) lane <= F) ? (ft & kValMask)
-                                                         : 0ull);
+                excl = wave_sum40((inq && (int) lane <= F) ? (ft & kValMask)
+                                                           : 0ull);
                 done = inc != 0;
                 break;
             }
@@ -529,7 +561,7 @@ struct LookBack
             const uint64_t upto = G >= 63 ? ~0ull : ((2ull << G) - 1);
             if ((inv & upto) == 0)
             {
-                excl += wave_sum((int) lane <= G ? (fv & kValMask) : 0ull);
+                excl += wave_sum40((int) lane <= G ? (fv & kValMask) : 0ull);
                 if (inc)
                     break;
                 fs = poll_super(c, ++back);
@@ -593,28 +625,19 @@ struct TileOut
         // bytes of tile chunk j - 1 and the first 16 - r of tile chunk j
         const uint32_t sh = (16 - r) & 15, q = sh >> 2, b = sh & 3;
         u32x4 g[NCH];
+        u32x4 rr[NCH];                       // lane i: lane i - 1 of o[j]
+#pragma unroll
+        for (int j = 0; j < NCH; ++j)
+            rr[j] = (u32x4){wave_ror1(o[j].x), wave_ror1(o[j].y),
+                            wave_ror1(o[j].z), wave_ror1(o[j].w)};
 #pragma unroll
         for (int j = 0; j < NCH; ++j)
         {
-            u32x4 prev;
-            prev.x = __shfl_up(o[j].x, 1, 64);
-            prev.y = __shfl_up(o[j].y, 1, 64);
-            prev.z = __shfl_up(o[j].z, 1, 64);
-            prev.w = __shfl_up(o[j].w, 1, 64);
-            if (j == 0)
-            {
-                if (lane == 0)
-                    prev = (u32x4){0, 0, 0, 0};
-            }
-            else
-            {
-                const u32x4 p63 = (u32x4){read_lane(o[j - 1].x, 63),
-                                          read_lane(o[j - 1].y, 63),
-                                          read_lane(o[j - 1].z, 63),
-                                          read_lane(o[j - 1].w, 63)};
-                if (lane == 0)
-                    prev = p63;
-            }
+            // lane 0 takes lane 63 of the chunk before (rotated into lane 0
+            // of rr[j - 1]), or zeros for the first
+            u32x4 prev = rr[j];
+            if (lane == 0)
+                prev = j ? rr[j - 1] : (u32x4){0, 0, 0, 0};
             const uint32_t d[8] = {prev.x, prev.y, prev.z, prev.w,
                                    o[j].x, o[j].y, o[j].z, o[j].w};
             // q is wave-uniform

@@ -54,7 +54,7 @@ struct EncSmem
                                      // 31 << 27 for longer codes
     uint8_t len[256];
     EncWave w[kWaves];
-    uint32_t tk[2];                  // the block's first two tickets
+    BlockTickets tk;                 // the workgroup's first tickets
 };
 
 // source of aligned input dwords: LDS stage or global
@@ -714,7 +714,7 @@ struct EncPolicy
             const uint32_t se = dense_at(wv, re);
             const uint32_t ra = (uint32_t) ((uintptr_t) (in + to.first()) - sp.pa);
             const uint32_t s_first = dense_at(wv, ra);
-            const uint32_t prev = __shfl_up(se, 1, 64);
+            const uint32_t prev = wave_shr1(se);
             ds = lane ? prev : s_first;
             bits = se - ds;
             dense = read_lane(se, cnt - 1) + 64 <= kDenseBits;
@@ -783,7 +783,7 @@ qhuff_encode_kernel(EncArgs a)
     clear_next_launch(a.c);
     Tickets tk;
     tk.init();
-    claim_block_tickets(a.c, tk, sm->tk);
+    claim_block_tickets(a.c, tk, &sm->tk);
     __syncthreads();                 // the only workgroup barrier
     EncPolicy pol;
     pol.in = a.in;
@@ -791,8 +791,9 @@ qhuff_encode_kernel(EncArgs a)
     pol.sm = sm;
     pol.wv = &sm->w[tid >> 6];
     pol.dense = false;
-    const uint32_t w = (uint32_t) (tid >> 6);
-    tile_pipeline(pol, a.c, tk, sm->tk[0] + w, sm->tk[1] + w, a.in, a.in_off,
+    uint32_t k0, k1;
+    wave_tickets(tk, &sm->tk, &k0, &k1);
+    tile_pipeline(pol, a.c, tk, k0, k1, a.in, a.in_off,
                   a.n, a.out, a.out_off, nullptr);
 }
 

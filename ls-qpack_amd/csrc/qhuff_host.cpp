@@ -181,11 +181,17 @@ struct qhuff_ctx
 // device words: [0] sticky error word (rest reserved)
 constexpr size_t kErrWords = 64;
 
+// the calling thread's last qhuff_open failure (qhuff_last_error(NULL))
+static thread_local char t_open_err[160] = "no context";
+
 static int
 fail(qhuff_ctx *c, hipError_t e, const char *what)
 {
     if (c)
+    {
         snprintf(c->err_msg, sizeof(c->err_msg), "%s: %s", what, hipGetErrorString(e));
+        snprintf(t_open_err, sizeof(t_open_err), "%s", c->err_msg);
+    }
     return e == hipErrorOutOfMemory ? QHUFF_ENOMEM : QHUFF_EDEVICE;
 }
 
@@ -235,7 +241,10 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         e = hash_occupancy(&occ_h);
     if (e != hipSuccess || occ_e < 1 || occ_d < 1 || occ_h < 1)
     {
-        rc = fail(c, e, "occupancy query");
+        char what[96];
+        snprintf(what, sizeof(what), "occupancy query (enc %d dec %d hash %d)",
+                 occ_e, occ_d, occ_h);
+        rc = fail(c, e, what);
         delete c;
         return rc ? rc : QHUFF_EDEVICE;
     }
@@ -337,7 +346,7 @@ qhuff_close(qhuff_ctx *c)
 extern "C" const char *
 qhuff_last_error(qhuff_ctx *c)
 {
-    return c ? c->err_msg : "no context";
+    return c ? c->err_msg : t_open_err;
 }
 
 extern "C" int

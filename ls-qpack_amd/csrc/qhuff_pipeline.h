@@ -18,12 +18,12 @@
 //          have the whole codec to land
 //   codec  P::prepare() (the encoder's byte-parallel pass over the stage),
 //          P::codec() -- LDS only -- per-lane output size (+ status)
-//   flush  one wait (the polls); resolve the older pending tile's look-back
-//          and store its output (registers)
 //   scan   wave scan -> tile-local offsets, tile total; publish the tile
 //          aggregate and add it to the super accumulator (LookBack::start)
-//   emit   P::emit() -- compacted output of t into the LDS out stage --
-//          gathered into registers (TileOut)
+//   emit   P::emit() -- compacted output of t into the LDS out stage
+//   flush  one wait (the polls, a codec and an emit ago); resolve the older
+//          pending tile's look-back and store its output (registers)
+//   gather t's output from the out stage into the freed registers (TileOut)
 //
 // Two tiles are pending at a time, both holding their output in registers:
 // tile k's look-back windows are polled at the top of iteration k + 2, a
@@ -86,21 +86,62 @@ wait_vm_all()
     __builtin_amdgcn_s_waitcnt(0x0f70);
 }
 
-// The kernel prologue claims each wave's first two tickets for the whole
-// block (one returning atomic per block and claim instead of one per wave:
-// ~3,000 waves claiming at once would queue on the counters)
-// (second-iteration tickets only when the grid's first claims cannot cover
-// every tile: a small batch then gets one tile per wave, not two per wave
-// of the first blocks to start)
-__device__ __forceinline__ void
-claim_block_tickets(const Coord &c, const Tickets &tk, QH_LDS uint32_t *base2)
+// The kernel prologue claims the first two tickets of every wave of the
+// workgroup: lanes 0..kTickGroups-1 of the first wave each take one group's
+// share with one returning atomic (~3,000 waves claiming one by one would
+// queue on the counters).  A wave of group g that is the r-th of its group
+// in the workgroup gets tickets base + r and base + n_g + r (n_g waves of
+// the workgroup in group g).  The second tickets only when the grid's first
+// claims cannot cover every tile (a small batch then gets one tile per wave,
+// not two per wave of the first workgroups to start); otherwise a sentinel
+// ticket whose tile lies past any batch.
+struct BlockTickets
 {
-    if (threadIdx.x == 0)
+    uint32_t base[kTickGroups];
+    uint32_t two;                    // second tickets claimed
+};
+
+__device__ __forceinline__ uint32_t
+tick_group_waves(uint32_t q)
+{
+    // waves w of this workgroup with (blockIdx.x * kWaves + w) % G == q
+    const uint32_t s = (blockIdx.x * (uint32_t) kWaves) % kTickGroups;
+    const uint32_t first = (q + kTickGroups - s) % kTickGroups;
+    return first < (uint32_t) kWaves
+         ? ((uint32_t) kWaves - 1 - first) / kTickGroups + 1 : 0u;
+}
+
+__device__ __forceinline__ void
+claim_block_tickets(const Coord &c, const Tickets &tk, QH_LDS BlockTickets *bt)
+{
+    const uint32_t t = threadIdx.x;
+    const bool two = (uint64_t) c.n_tiles > (uint64_t) gridDim.x * kWaves;
+    if (t < kTickGroups)
     {
-        base2[0] = tk.claim_many(c, kWaves);
-        base2[1] = (uint64_t) c.n_tiles > (uint64_t) gridDim.x * kWaves
-                 ? tk.claim_many(c, kWaves) : 0xffffffffu / kTickGroups;
+        const uint32_t nq = tick_group_waves(t);
+        uint32_t b = 0;
+        if (nq)
+            b = __hip_atomic_fetch_add(tk.counter(c, t), two ? 2 * nq : nq,
+                                       __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        bt->base[t] = b;
     }
+    if (t == 0)
+        bt->two = two ? 1u : 0u;
+}
+
+// this wave's first two tickets (after the workgroup barrier)
+__device__ __forceinline__ void
+wave_tickets(const Tickets &tk, const QH_LDS BlockTickets *bt, uint32_t *k0,
+             uint32_t *k1)
+{
+    // rank among this workgroup's waves of the same group (waves w and
+    // w + kTickGroups share one)
+    const uint32_t r = (threadIdx.x >> 6) / kTickGroups;
+    const uint32_t nq = tick_group_waves(tk.g);
+    *k0 = bt->base[tk.g] + r;
+    *k1 = bt->two ? bt->base[tk.g] + nq + r
+                  : 0xffffffffu / kTickGroups - kWaves;   // tile past the end
 }
 
 template <class P>
@@ -195,7 +236,25 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         fast = fast && total + 64 <= (uint32_t) kStageCap;
         prof_stamp(c, it, 3);
 
-        // the polls (a codec ago); resolve + store the older tile
+        Pending cur;
+        cur.valid = false;
+        if (fast)
+        {
+            // publish t's aggregate, pack t into the LDS out stage
+            cur.valid = true;
+            cur.tile = t;
+            cur.cnt = cnt;
+            cur.total = total;
+            cur.excl = excl;
+            cur.stat = st;
+            cur.lb.start(c, t, total);
+            wave_sync();
+            pol.emit(excl, sz, total);
+            wave_sync();
+        }
+        prof_stamp(c, it, 9);
+
+        // the polls (a codec and an emit ago); resolve + store the older tile
         wait_vm_all();
         prof_stamp(c, it, 4);
         if (older.valid)
@@ -203,24 +262,11 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
                                    n, it);
         older = newer;
         older_out = newer_out;
-        newer.valid = false;
+        newer = cur;
         prof_stamp(c, it, 5);
 
         if (fast)
-        {
-            newer.valid = true;
-            newer.tile = t;
-            newer.cnt = cnt;
-            newer.total = total;
-            newer.excl = excl;
-            newer.stat = st;
-            newer.lb.start(c, t, total);
-            wave_sync();
-            pol.emit(excl, sz, total);
-            wave_sync();
-            prof_stamp(c, it, 9);
             newer_out.gather(pol.out_stage());
-        }
         else
         {
             if (older.valid)

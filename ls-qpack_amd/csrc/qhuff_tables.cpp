@@ -79,12 +79,12 @@ build_tables(HostTables *t)
         uint32_t e = 0;
         if (s0 >= 0 && s0 < 256)
         {
-            e = (uint32_t) s0 | ((uint32_t) l0 << 16) | ((uint32_t) l0 << 20)
+            e = (uint32_t) s0 | ((uint32_t) l0 << 8) | ((uint32_t) l0 << 12)
               | (1u << 24) | ((uint32_t) (32 - l0) << 26);
             int s1 = canon_decode(&c, left << l0, kWinBits - l0, &l1);
             if (s1 >= 0 && s1 < 256)
-                e = (uint32_t) s0 | ((uint32_t) s1 << 8)
-                  | ((uint32_t) (l0 + l1) << 16) | ((uint32_t) l0 << 20)
+                e = (uint32_t) s0 | ((uint32_t) s1 << 16)
+                  | ((uint32_t) (l0 + l1) << 8) | ((uint32_t) l0 << 12)
                   | (2u << 24) | ((uint32_t) (32 - l0 - l1) << 26);
         }
         t->win[w] = e;

@@ -29,10 +29,12 @@ constexpr int kWinBits = QH_WIN_BITS;
 constexpr int kWinSize = 1 << kWinBits;
 constexpr int kMaxLong = 16;            // lengths 13..30 that occur (14 used)
 
-// window entry: sym0 [7:0] | sym1 [15:8] | bits consumed by all nsym
-//               symbols c [19:16] | len0 [23:20] | nsym [25:24] |
+// window entry: sym0 [7:0] | bits consumed by all nsym symbols c [11:8] |
+//               len0 [15:12] | sym1 [23:16] | nsym [25:24] |
 //               32 - c [31:26] (the decoder's alignbit shift); nsym == 0:
-//               the first code is longer than 12 bits (entry < 1 << 24)
+//               the first code is longer than the window (entry < 1 << 24).
+//               sym1 sits at [23:16] so the decoder stores it with
+//               ds_write_b8_d16_hi, no shift.
 struct LongLen { uint32_t len, first, count, base; };
 
 // RFC 7541 Appendix B code lengths, symbols 0..256 (EOS = 256).

@@ -79,6 +79,15 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise QhuffError("libqhuff.so not built: run make -C %s" % PKG_ROOT)
+        # One HIP runtime per process: PyTorch ships its own libamdhip64
+        # (NEEDED as "libamdhip64.so", soname libamdhip64.so.7).  Loaded
+        # first, it satisfies libqhuff's libamdhip64.so.7 dependency; loaded
+        # after libqhuff it would be a second runtime (the GPU appears twice,
+        # occupancy queries and torch.cuda break).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         vp, u32p = C.c_void_p, C.c_void_p
         L.qhuff_open.restype = C.c_int
@@ -281,7 +290,8 @@ class Codec:
         self._ctx = C.c_void_p()
         rc = lib().qhuff_open(device, C.byref(self._ctx))
         if rc != OK:
-            raise QhuffError("qhuff_open(device=%d) failed: %d" % (device, rc))
+            raise QhuffError("qhuff_open(device=%d) failed: %d (%s)" % (
+                device, rc, lib().qhuff_last_error(None).decode()))
         self.device = device
 
     def close(self):

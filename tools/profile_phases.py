@@ -2,9 +2,9 @@
 """Per-phase cycle breakdown of the wave pipeline from a QHUFF_PROFILE build
 (make -C ls-qpack_amd prof; run with QHUFF_LIB=.../libqhuff_prof.so).
 Slots per wave iteration (qhuff_pipeline.h): 0 top, 1 after the top wait,
-2 after stage + loads + polls, 3 after codec + scan, 4 after the poll wait,
-7 after the older tile's look-back (inside the flush), 5 after the flush,
-9 after lb.start + emit, 6 end of iteration (after the gather)."""
+2 after stage + loads + polls, 3 after codec + scan, 9 after lb.start +
+emit, 4 after the poll wait, 7 after the older tile's look-back (inside the
+flush), 5 after the flush, 6 end of iteration (after the gather)."""
 import os
 import sys
 
@@ -18,8 +18,8 @@ import torch
 import qhuff
 
 ITERS, SLOTS = 16, 12
-NAMES = ["top wait", "stage+loads+polls", "codec+scan", "poll wait",
-         "flush", "start+emit+gather"]
+NAMES = ["top wait", "stage+loads+polls", "codec+scan", "start+emit+wait",
+         "flush", "gather"]
 
 
 def report(tag, p):
@@ -45,11 +45,11 @@ def report(tag, p):
         print("  flush: look-back mean %.0f p90 %.0f | stores mean %.0f | re-polls mean %.2f, >0 in %.1f%%, max %d"
               % (lbt.mean(), np.percentile(lbt, 90), stt.mean(), sp.mean(),
                  100.0 * (sp > 0).mean(), sp.max()))
-    ok = live & (p[:, :, 5] != 0) & (p[:, :, 9] != 0)
+    ok = live & (p[:, :, 3] != 0) & (p[:, :, 9] != 0) & (p[:, :, 4] != 0)
     if ok.any():
-        a = (p[:, :, 9] - p[:, :, 5])[ok]
-        b = (p[:, :, 6] - p[:, :, 9])[ok]
-        print("  start+emit mean %.0f p90 %.0f | gather mean %.0f p90 %.0f"
+        a = (p[:, :, 9] - p[:, :, 3])[ok]
+        b = (p[:, :, 4] - p[:, :, 9])[ok]
+        print("  start+emit mean %.0f p90 %.0f | poll wait mean %.0f p90 %.0f"
               % (a.mean(), np.percentile(a, 90), b.mean(), np.percentile(b, 90)))
     if not os.environ.get("TIMELINE"):
         return
