@@ -34,7 +34,16 @@ __device__ __forceinline__ uint32_t ent_l0(uint32_t e) { return (e >> 12) & 15; 
 __device__ __forceinline__ uint32_t ent_ns(uint32_t e) { return (e >> 24) & 3; }
 __device__ __forceinline__ uint32_t ent_sym1(uint32_t e) { return (e >> 16) & 0xff; }
 
-constexpr int kDecInCap = kStageCap;                   // staged input bytes
+// staged input bytes (the output stage, the dead input stage, always has the
+// chunk registers' 3,072).  2,816 lets 16 waves (4 per SIMD, <= 128 VGPRs)
+// fit the LDS -- measured slower than 12 waves (dec 88 vs 86 us: the codec
+// is issue-bound and the look-backs wait longer), so the default is the
+// full 3,072 at 12 waves.
+#ifndef QH_DEC_IN_CAP
+#define QH_DEC_IN_CAP 3072
+#endif
+constexpr int kDecInCap = QH_DEC_IN_CAP;
+static_assert(kDecInCap % 16 == 0 && kDecInCap <= kStageCap, "input cap");
 // byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
 // most 8/5 of its input, plus one byte written past the end by the
 // two-byte emitter
@@ -42,7 +51,7 @@ constexpr int kArenaBytes = 2 * kWT + 8 * kDecInCap / 5 + 32;
 
 struct DecWave                       // one wave's private LDS region
 {
-    alignas(16) uint32_t in[kDecInCap / 4];   // BE input dwords; output stage
+    alignas(16) uint32_t in[kStageCap / 4];   // BE input dwords; output stage
     alignas(16) uint8_t arena[kArenaBytes];
 };
 
@@ -482,6 +491,8 @@ dec_slow_tile(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
 struct DecPolicy
 {
     static constexpr bool kStatus = true;
+    static constexpr int kInCap = kDecInCap;
+    static constexpr int kOutCap = kStageCap;
     const uint8_t *in;
     QH_LDS DecSmem *sm;
     QH_LDS DecWave *wv;

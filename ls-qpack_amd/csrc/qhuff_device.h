@@ -25,6 +25,9 @@ namespace qhuff {
 #define QH_LDS __attribute__((address_space(3)))
 #define QH_GLB __attribute__((address_space(1)))
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// byte-aligned views for unaligned global stores (gfx9 unaligned mode)
+struct __attribute__((packed, aligned(1))) U4 { u32x4 v; };
+struct __attribute__((packed, aligned(1))) U1 { uint32_t v; };
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWT = 64;                     // strings per wave tile
@@ -431,7 +434,7 @@ struct LookBack
     uint32_t tile, s;
     uint32_t total;
     uint64_t acc_old;            // returned by the super accumulator add (lane 0)
-    uint64_t ft, fs;             // polled tile / super flags (one per lane)
+    uint64_t ft, fs, fs1;        // polled tile flags, super flags back 0 / 1
     uint32_t spins_seen;         // re-polls of the last finish() (profiling)
 
     __device__ __forceinline__ static uint64_t ep(const Coord &c)
@@ -499,10 +502,15 @@ struct LookBack
         if ((old >> 48) == in_super - 1)
             publish_super(c, kFlagAgg, (old + total) & kAccMask);
     }
+    // the tile window and two super windows (128 super tiles): with ~2
+    // iterations of ~3,000-4,000 waves between a tile's codec and its
+    // inclusive flag, the nearest inclusive super flag is 100-130 super tiles
+    // back, so one window would cost a second round trip on most tiles
     __device__ __forceinline__ void poll(const Coord &c)
     {
         ft = poll_tile(c);
         fs = poll_super(c, 0);
+        fs1 = poll_super(c, 1);
     }
 
     __device__ __forceinline__ bool spin(const Coord &c, uint32_t *spins) const
@@ -564,7 +572,9 @@ struct LookBack
                 excl += wave_sum40((int) lane <= G ? (fv & kValMask) : 0ull);
                 if (inc)
                     break;
-                fs = poll_super(c, ++back);
+                ++back;
+                // the second window was polled with the first
+                fs = back == 1 ? fs1 : poll_super(c, back);
                 continue;
             }
             if (!spin(c, &spins))
@@ -613,81 +623,47 @@ struct TileOut
             ((QH_LDS u32x4 *) hold)[lane + 64 * j] = o[j];
     }
 
+    // Global stores of the tile's `total` bytes at dst (any alignment: the
+    // ROCm driver runs gfx9 in unaligned-access mode, and the 16-byte stores
+    // of neighbouring lanes and tiles never overlap).  Whole 16-byte chunks:
+    // one dwordx4 store per lane; the partial last chunk: its owner lane
+    // writes its whole dwords, then its last 0-3 bytes.
     __device__ __forceinline__ void store(uint8_t *dst, uint32_t total) const
     {
         const uint32_t lane = lane_id();
-        const uint32_t r = (uint32_t) ((uintptr_t) dst & 15);
-        // wave-uniform 16-byte aligned base, 32-bit lane offsets
-        QH_GLB u32x4 *g4 = (QH_GLB u32x4 *) (dst - r);
-        QH_GLB uint8_t *g1 = (QH_GLB uint8_t *) (dst - r);
-        const uint32_t nch = total ? (r + total + 15) >> 4 : 0;  // global chunks
-        // global chunk j = tile bytes [16 j - r, 16 j - r + 16): the last r
-        // bytes of tile chunk j - 1 and the first 16 - r of tile chunk j
-        const uint32_t sh = (16 - r) & 15, q = sh >> 2, b = sh & 3;
-        u32x4 g[NCH];
-        u32x4 rr[NCH];                       // lane i: lane i - 1 of o[j]
-#pragma unroll
-        for (int j = 0; j < NCH; ++j)
-            rr[j] = (u32x4){wave_ror1(o[j].x), wave_ror1(o[j].y),
-                            wave_ror1(o[j].z), wave_ror1(o[j].w)};
-#pragma unroll
-        for (int j = 0; j < NCH; ++j)
-        {
-            // lane 0 takes lane 63 of the chunk before (rotated into lane 0
-            // of rr[j - 1]), or zeros for the first
-            u32x4 prev = rr[j];
-            if (lane == 0)
-                prev = j ? rr[j - 1] : (u32x4){0, 0, 0, 0};
-            const uint32_t d[8] = {prev.x, prev.y, prev.z, prev.w,
-                                   o[j].x, o[j].y, o[j].z, o[j].w};
-            // q is wave-uniform
-            switch (r == 0 ? 4 : q)
-            {
-            case 0: g[j] = (u32x4){align_bytes(d[1], d[0], b), align_bytes(d[2], d[1], b),
-                                   align_bytes(d[3], d[2], b), align_bytes(d[4], d[3], b)}; break;
-            case 1: g[j] = (u32x4){align_bytes(d[2], d[1], b), align_bytes(d[3], d[2], b),
-                                   align_bytes(d[4], d[3], b), align_bytes(d[5], d[4], b)}; break;
-            case 2: g[j] = (u32x4){align_bytes(d[3], d[2], b), align_bytes(d[4], d[3], b),
-                                   align_bytes(d[5], d[4], b), align_bytes(d[6], d[5], b)}; break;
-            case 3: g[j] = (u32x4){align_bytes(d[4], d[3], b), align_bytes(d[5], d[4], b),
-                                   align_bytes(d[6], d[5], b), align_bytes(d[7], d[6], b)}; break;
-            default: g[j] = o[j]; break;
-            }
-        }
-        const bool last_part = ((r + total) & 15) != 0;
-        const bool first_part = r != 0 || (nch == 1 && last_part);
+        const uint32_t nfull = total >> 4, rem = total & 15;
+        // (compile-time chunk index j throughout: a run-time select between
+        // the o[] would put the array in scratch memory)
 #pragma unroll
         for (int j = 0; j < NCH; ++j)
         {
             const uint32_t k = lane + 64u * j;
-            const bool part = (k == 0 && first_part) || (k == nch - 1 && last_part);
-            if (k < nch && !part)
-                g4[k] = g[j];
+            if (k < nfull)
+                ((QH_GLB U4 *) (dst + 16u * k))->v = o[j];
+            else if (k == nfull && rem)
+                store_part(dst + 16u * k, o[j], rem);
         }
-        // partial chunks: lanes 0-15 write bytes of chunk 0, lanes 16-31 bytes
-        // of chunk nch - 1 (when it is another partial chunk)
-        const uint32_t kl = nch ? nch - 1 : 0, jl = kl >> 6, ll = kl & 63;
-        u32x4 cl = g[0];
-#pragma unroll
-        for (int j = 1; j < NCH; ++j)
-            cl = jl == (uint32_t) j ? g[j] : cl;
-        const u32x4 c0 = (u32x4){read_lane(g[0].x, 0), read_lane(g[0].y, 0),
-                                 read_lane(g[0].z, 0), read_lane(g[0].w, 0)};
-        const u32x4 cz = (u32x4){read_lane(cl.x, ll), read_lane(cl.y, ll),
-                                 read_lane(cl.z, ll), read_lane(cl.w, ll)};
-        const bool lo_half = lane < 16;
-        const uint32_t bi = lane & 15;
-        const uint32_t kk = lo_half ? 0 : kl;
-        const u32x4 src = lo_half ? c0 : cz;
-        const uint32_t wsel = bi >> 2;
-        const uint32_t wv = wsel == 0 ? src.x : wsel == 1 ? src.y
-                          : wsel == 2 ? src.z : src.w;
-        const uint32_t gb = 16 * kk + bi;            // byte offset from g0
-        const bool in_range = gb >= r && gb < r + total;
-        const bool want = lane < 32 && in_range
-                       && (lo_half ? first_part : (last_part && kl != 0));
-        if (want)
-            g1[gb] = (uint8_t) (wv >> (8 * (bi & 3)));
+    }
+    __device__ __forceinline__ static void store_part(uint8_t *dst, u32x4 v,
+                                                      uint32_t rem)
+    {
+        QH_GLB uint8_t *p = (QH_GLB uint8_t *) dst;
+        const uint32_t nd = rem >> 2;
+        if (nd > 0)
+            ((QH_GLB U1 *) p)->v = v.x;
+        if (nd > 1)
+            ((QH_GLB U1 *) (p + 4))->v = v.y;
+        if (nd > 2)
+            ((QH_GLB U1 *) (p + 8))->v = v.z;
+        const uint32_t wt = nd == 0 ? v.x : nd == 1 ? v.y : nd == 2 ? v.z : v.w;
+        const uint32_t nb = rem & 3;
+        QH_GLB uint8_t *q = p + 4 * nd;
+        if (nb > 0)
+            q[0] = (uint8_t) wt;
+        if (nb > 1)
+            q[1] = (uint8_t) (wt >> 8);
+        if (nb > 2)
+            q[2] = (uint8_t) (wt >> 16);
     }
 };
 

@@ -673,6 +673,8 @@ enc_slow_tile(const uint8_t *in, uint32_t mode, QH_LDS EncSmem *sm,
 struct EncPolicy
 {
     static constexpr bool kStatus = false;
+    static constexpr int kInCap = kEncInCap;
+    static constexpr int kOutCap = kEncOutCap;
     const uint8_t *in;
     uint32_t mode;                   // 0 payload, 3/5/7 literal prefix bits
     QH_LDS EncSmem *sm;

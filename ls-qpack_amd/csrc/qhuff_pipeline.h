@@ -39,7 +39,7 @@
 namespace qhuff {
 
 constexpr int kChunks = 3;                  // 16-byte input chunks per lane
-constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: input / output stage
+constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: chunk registers / stages
 
 // A coded tile waiting for its look-back: per-lane output offset and status,
 // the look-back state; its output bytes wait in registers (TileOut).
@@ -177,7 +177,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     // once tn is past the end every later claim is too)
     const uint32_t kNone = 0xffffffffu;
     uint32_t kq = tn < nt ? tk.claim(c) : kNone;
-    Span sp_cur = tile_span(in, o_cur.first(), o_cur.last(), kStageCap);
+    Span sp_cur = tile_span(in, o_cur.first(), o_cur.last(), P::kInCap);
     Chunks<kChunks> ch;
     ch.load(sp_cur);
 
@@ -212,7 +212,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         // of tn, offsets of the ticketed tile after it, the next ticket; the
         // older pending tile's look-back polls
         const uint32_t tnn = tn < nt ? tk.tile_of(kq) : kNone;
-        const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), kStageCap);
+        const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), P::kInCap);
         ch.load(sp_nxt);
         const uint32_t tz = clamp(tnn);
         o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
@@ -233,7 +233,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         const uint32_t incl = wave_incl_scan(sz);
         const uint32_t excl = incl - sz;
         const uint32_t total = read_lane(incl, 63);
-        fast = fast && total + 64 <= (uint32_t) kStageCap;
+        fast = fast && total + 64 <= (uint32_t) P::kOutCap;
         prof_stamp(c, it, 3);
 
         Pending cur;
