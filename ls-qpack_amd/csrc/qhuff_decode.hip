@@ -26,6 +26,10 @@
 // tile's output base.
 #include "qhuff_pipeline.h"
 
+#ifndef QH_DEPTH
+#define QH_DEPTH 3
+#endif
+
 namespace qhuff {
 
 // window entry fields (qhuff_tables.h)
@@ -492,6 +496,7 @@ struct DecPolicy
 {
     static constexpr bool kStatus = true;
     static constexpr int kInCap = kDecInCap;
+    static constexpr int kDepth = QH_DEPTH;       // pending tiles
     static constexpr int kOutCap = kStageCap;
     const uint8_t *in;
     QH_LDS DecSmem *sm;

@@ -31,6 +31,10 @@
 // (global reads / per-lane global writes).
 #include "qhuff_pipeline.h"
 
+#ifndef QH_DEPTH
+#define QH_DEPTH 2
+#endif
+
 namespace qhuff {
 
 constexpr int kEncInCap = kStageCap;          // staged input bytes per tile
@@ -674,6 +678,7 @@ struct EncPolicy
 {
     static constexpr bool kStatus = false;
     static constexpr int kInCap = kEncInCap;
+    static constexpr int kDepth = QH_DEPTH;       // pending tiles
     static constexpr int kOutCap = kEncOutCap;
     const uint8_t *in;
     uint32_t mode;                   // 0 payload, 3/5/7 literal prefix bits

@@ -25,10 +25,13 @@
 //          pending tile's look-back and store its output (registers)
 //   gather t's output from the out stage into the freed registers (TileOut)
 //
-// Two tiles are pending at a time, both holding their output in registers:
-// tile k's look-back windows are polled at the top of iteration k + 2, a
-// whole iteration after every tile before it published its aggregate, and
-// resolved after that iteration's codec.
+// P::kDepth tiles are pending at a time, all holding their output in
+// registers: tile k's look-back windows are polled at the top of iteration
+// k + kDepth, kDepth - 1 whole iterations after every tile before it
+// published its aggregate, and resolved after that iteration's codec and
+// emit.  (A wave held up in a look-back delays its own next codecs, and so
+// the look-backs of the tiles after those: the deeper the pipeline, the more
+// slack before such a delay propagates.)
 //
 // Tiles whose input or output does not fit the stages are coded eagerly by
 // P::slow_tile() (out of line) after the pending tiles have been flushed.
@@ -181,17 +184,19 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     Chunks<kChunks> ch;
     ch.load(sp_cur);
 
-    // Two tiles are pending at a time.  Tile k's look-back is resolved at
-    // the top of iteration k + 2; its windows are polled at the end of
-    // iteration k + 1, a whole codec after every tile before it published
-    // its aggregate.  Tiles come from in-order tickets claimed two
-    // iterations ahead (one claim per wave per iteration), so the order in
-    // which tiles are claimed is the order in which they are coded, and a
-    // look-back only ever waits on tiles held by running waves.  Between its
-    // codec and its store a tile's output sits in registers.
-    Pending older, newer;
-    older.valid = newer.valid = false;
-    TileOut<kChunks> older_out, newer_out;
+    // Tiles come from in-order tickets claimed two iterations ahead (one
+    // claim per wave per iteration), so the order in which a wave claims
+    // tiles is the order in which it codes them, and a look-back only ever
+    // waits on tiles held by running waves.  Between its codec and its
+    // store a tile's output sits in registers: P::kDepth pending tiles,
+    // oldest first (compile-time indices only: the arrays stay in
+    // registers).
+    constexpr int D = P::kDepth;
+    Pending pend[D];
+    TileOut<kChunks> outs[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+        pend[i].valid = false;
     uint32_t it = 0;
     for (;; ++it)
     {
@@ -200,25 +205,25 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         // iteration's stores and look-back start (an emit ago)
         wait_vm_all();
         prof_stamp(c, it, 1);
-        // the newer tile's add has returned: publish the super aggregate if
-        // it completed its super tile (as early as possible: look-backs of
-        // later super tiles wait on it)
-        if (newer.valid)
-            newer.lb.super_agg(c);
+        // the newest pending tile's add has returned: publish the super
+        // aggregate if it completed its super tile (as early as possible:
+        // look-backs of later super tiles wait on it)
+        if (pend[D - 1].valid)
+            pend[D - 1].lb.super_agg(c);
         if (sp_cur.staged)
             pol.stage_in(ch, sp_cur, o_cur);
         wave_sync();
         // loads for the next tiles, a whole codec ahead of their use: input
         // of tn, offsets of the ticketed tile after it, the next ticket; the
-        // older pending tile's look-back polls
+        // oldest pending tile's look-back polls
         const uint32_t tnn = tn < nt ? tk.tile_of(kq) : kNone;
         const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), P::kInCap);
         ch.load(sp_nxt);
         const uint32_t tz = clamp(tnn);
         o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
         kq = tnn < nt ? tk.claim(c) : kNone;
-        if (older.valid)
-            older.lb.poll(c);
+        if (pend[0].valid)
+            pend[0].lb.poll(c);
         prof_stamp(c, it, 2);
 
         // codec of t (LDS only when staged)
@@ -254,26 +259,36 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         }
         prof_stamp(c, it, 9);
 
-        // the polls (a codec and an emit ago); resolve + store the older tile
+        // the polls (a codec and an emit ago); resolve + store the oldest
         wait_vm_all();
         prof_stamp(c, it, 4);
-        if (older.valid)
-            flush_tile<P::kStatus>(c, older, older_out, out, out_off, status,
+        if (pend[0].valid)
+            flush_tile<P::kStatus>(c, pend[0], outs[0], out, out_off, status,
                                    n, it);
-        older = newer;
-        older_out = newer_out;
-        newer = cur;
+#pragma unroll
+        for (int i = 0; i + 1 < D; ++i)
+        {
+            pend[i] = pend[i + 1];
+            outs[i] = outs[i + 1];
+        }
+        pend[D - 1] = cur;
         prof_stamp(c, it, 5);
 
         if (fast)
-            newer_out.gather(pol.out_stage());
+            outs[D - 1].gather(pol.out_stage());
         else
         {
-            if (older.valid)
-            {
-                older.lb.poll(c);
-                flush_tile<P::kStatus>(c, older, older_out, out, out_off, status, n);
-            }
+            // (a slow tile only needs its predecessors' aggregates; the
+            // pending tiles are flushed first so that no tile output is live
+            // across the out-of-line call)
+#pragma unroll
+            for (int i = 0; i < D; ++i)
+                if (pend[i].valid)
+                {
+                    pend[i].lb.poll(c);
+                    flush_tile<P::kStatus>(c, pend[i], outs[i], out, out_off,
+                                           status, n);
+                }
             pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
                           status, n);
         }
@@ -289,18 +304,15 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         sp_cur = sp_nxt;
     }
     wait_vm_all();
-    if (newer.valid)
-        newer.lb.super_agg(c);
-    if (older.valid)
-    {
-        older.lb.poll(c);
-        flush_tile<P::kStatus>(c, older, older_out, out, out_off, status, n);
-    }
-    if (newer.valid)
-    {
-        newer.lb.poll(c);
-        flush_tile<P::kStatus>(c, newer, newer_out, out, out_off, status, n);
-    }
+    if (pend[D - 1].valid)
+        pend[D - 1].lb.super_agg(c);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+        if (pend[i].valid)
+        {
+            pend[i].lb.poll(c);
+            flush_tile<P::kStatus>(c, pend[i], outs[i], out, out_off, status, n);
+        }
 }
 
 }  // namespace qhuff
