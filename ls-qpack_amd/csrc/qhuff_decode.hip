@@ -558,21 +558,38 @@ qhuff_decode_kernel(DecArgs a)
     __shared__ DecSmem smem;
     QH_LDS DecSmem *sm = (QH_LDS DecSmem *) &smem;
     const int tid = threadIdx.x;
+    Tickets tk;
+    tk.init();
     {
+        // every load of the tables issued before the first LDS store (one
+        // memory round trip, not one per loop trip), the ticket claims
+        // beside them
+        constexpr int kPer = (kWinSize / 4 + 64 * kWaves - 1) / (64 * kWaves);
         const QH_GLB u32x4 *gw = (const QH_GLB u32x4 *) glb(a.win);
         QH_LDS u32x4 *sw = (QH_LDS u32x4 *) sm->win;
-        for (int i = tid; i < kWinSize / 4; i += 64 * kWaves)
-            sw[i] = gw[i];
+        u32x4 v[kPer];
+#pragma unroll
+        for (int r = 0; r < kPer; ++r)
+        {
+            const int i = tid + r * 64 * kWaves;
+            v[r] = gw[i < kWinSize / 4 ? i : 0];
+        }
         const QH_GLB uint16_t *gs = glb(a.sorted);
+        const uint16_t so = gs[tid < 257 ? tid : 0];
+        claim_block_tickets(a.c, tk, &sm->tk);
+#pragma unroll
+        for (int r = 0; r < kPer; ++r)
+        {
+            const int i = tid + r * 64 * kWaves;
+            if (i < kWinSize / 4)
+                sw[i] = v[r];
+        }
         if (tid < 257)
-            sm->sorted[tid] = gs[tid];
+            sm->sorted[tid] = so;
         if (tid == 0)
             sm->win[kHoldIdx] = kHoldEntry;
         clear_next_launch(a.c);
     }
-    Tickets tk;
-    tk.init();
-    claim_block_tickets(a.c, tk, &sm->tk);
     __syncthreads();                 // the only workgroup barrier
     DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
     uint32_t k0, k1;
