@@ -88,6 +88,13 @@ def test_one_context_two_streams(batch):
         c.encode_into(d, o, n, 0, eo, eoo, s)          # caller stream
         ho2, hoo2 = c.encode_host(data, off, 0)          # own stream, no sync
         dr, droo, dst = c.decode_host(h, ho)             # own stream
+        c.encode_into(d, o, n, 0, eo, eoo, s)          # caller stream again
+        # per-string calls right behind it, no sync
+        s1 = bytes(data[off[5]:off[6]])
+        assert c.enc_enc_str(7, s1) == O.enc_enc_str(7, s1)
+        e1 = O.huffman_enc(s1)
+        st1, out1, n1 = c.huff_decode(e1)
+        assert (st1, out1, n1) == (0, s1, len(e1))
         s.synchronize()
         assert np.array_equal(hoo2, ho) and np.array_equal(ho2, h)
         assert np.array_equal(droo, off) and not dst.any()
