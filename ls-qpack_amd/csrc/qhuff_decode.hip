@@ -255,16 +255,20 @@ decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
     return bad ? -1 : (int) emit.n;
 }
 
-// Lean variant used by the staged (LDS) path.  The bit buffer is one 64-bit
-// register, MSB = next bit, holding >= 32 valid bits at every main step; the
-// dword that refills it is read beside the table lookup, so only the lookup
-// sits on the step's dependency chain.  Main steps run while a lane has at
-// least kWinBits real bits left, so the window holds no padding and every
-// symbol of its entry is real (a lane past that reads the hold entry: it
-// consumes and emits nothing); the EOS check and the "code runs past the
-// end" check (the leftover would be >= 8 bits: D3) live in the rare long-code
-// branch.  The last < kWinBits bits (at most two symbols) take the padded
-// epilogue with the D3 tail rule, exactly as decode_string().
+// Lean variant used by the staged (LDS) path.  The bit stream sits in two
+// dwords A:B with a position t: the 32-bit window is alignbit(A, B, t) --
+// ((A:B) >> t), the next bit at A's bit 31 - (32 - t) -- valid for t in
+// [0, 31] (t = 0: the window is B).  Consuming c bits lowers t; when it goes
+// negative the window moves on a dword (A = B, B = the next dword, read one
+// step ahead) and t wraps (t & 31).  No 64-bit shifts, and the window always
+// holds 32 stream bits, enough for any code.  Main steps run while a lane
+// has at least kWinBits real bits left, so the window's top kWinBits bits
+// hold no padding and every symbol of its entry is real (a lane past that
+// reads the hold entry: it consumes and emits nothing); the EOS check and
+// the "code runs past the end" check (the leftover would be >= 8 bits: D3)
+// live in the rare long-code branch.  The last < kWinBits bits (at most two
+// symbols) take the padded epilogue with the D3 tail rule, exactly as
+// decode_string().
 template <class Emit>
 __device__ __forceinline__ int
 decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
@@ -272,14 +276,14 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
                   Emit &emit)
 {
     uint32_t rem = bitend - bit0;            // real bits not yet consumed
-    uint64_t buf = 0;
-    uint32_t bits = 0, p = 0, nx = 0;
+    uint32_t A, B, t, p, nx;
     {
         const uint32_t i0 = bit0 >> 5, sk = bit0 & 31;
-        const uint64_t ab = ((uint64_t) src[i0] << 32) | src[i0 + 1];
-        buf = ab << sk;
-        bits = 64 - sk;
-        p = i0 + 2;
+        A = src[i0];
+        const uint32_t a1 = src[i0 + 1];
+        B = sk ? a1 : A;                     // sk == 0: the window is B = A
+        t = (32 - sk) & 31;
+        p = sk ? i0 + 2 : i0 + 1;
         nx = src[p];
     }
     uint32_t bad = 0;                        // (a u32: no lane-mask phis)
@@ -287,27 +291,23 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
     // looks up the hold entry (c = ns = 0, never a long code); its two arena
     // byte writes land at its current end and are overwritten by the
     // epilogue.  The long-code fix is computed for the whole wave with
-    // selects, behind a wave-uniform branch.  The next window is taken from
-    // the shifted buffer BEFORE the refill: a step of <= 13 bits leaves >= 19
-    // valid bits, so the step's dependency chain is lookup -> length ->
-    // shift -> index, with the refill beside it (after a long code the index
-    // is recomputed behind a second uniform branch).
+    // selects, behind a wave-uniform branch.
     constexpr uint32_t kMain = kWinBits;
-    uint32_t idx = rem >= kMain ? (uint32_t) (buf >> (64 - kWinBits)) : kHoldIdx;
+    uint32_t W = __builtin_amdgcn_alignbit(A, B, t);
+    uint32_t idx = rem >= kMain ? W >> (32 - kWinBits) : kHoldIdx;
     if (__builtin_amdgcn_ballot_w64(rem >= kMain))
     do
     {
         uint32_t e = s_win[idx];
         uint32_t c = ent_c(e);                // bits of the entry's symbols
         uint32_t ns = ent_ns(e);              // symbols (0: longer code)
-        const bool any_long = __builtin_amdgcn_ballot_w64(e < (1u << 24)) != 0;
-        if (any_long)
+        if (__builtin_amdgcn_ballot_w64(e < (1u << 24)))
         {
             // a code of 14..30 bits; EOS, or a code running past the end,
             // rejects the string (D3)
             const bool lng = e < (1u << 24);
             uint32_t L;
-            const uint32_t sym = long_code((uint32_t) (buf >> 32), s_sorted, &L);
+            const uint32_t sym = long_code(W, s_sorted, &L);
             const bool rej = lng & ((sym == 256) | (L > rem));
             e = lng ? sym : e;
             c = lng ? (rej ? 0u : L) : c;
@@ -315,20 +315,17 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
             bad |= rej ? 1u : 0u;
             rem = rej ? 0u : rem;
         }
-        buf <<= c;
-        idx = (uint32_t) (buf >> (64 - kWinBits));
         emit(e, ns);
-        bits -= c;
         rem -= c;
-        const bool need = bits < 32;
-        const uint32_t dd = need ? nx : 0u;
-        buf |= (uint64_t) dd << ((32 - bits) & 31);
-        bits += need ? 32u : 0u;
-        p += need ? 1u : 0u;
+        const int32_t tn = (int32_t) t - (int32_t) c;
+        const bool cross = tn < 0;
+        A = cross ? B : A;
+        B = cross ? nx : B;
+        t = (uint32_t) tn & 31;
+        p += cross ? 1u : 0u;
         nx = src[p];
-        if (any_long)
-            idx = (uint32_t) (buf >> (64 - kWinBits));
-        idx = rem >= kMain ? idx : kHoldIdx;
+        W = __builtin_amdgcn_alignbit(A, B, t);
+        idx = rem >= kMain ? W >> (32 - kWinBits) : kHoldIdx;
     } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
 
     // epilogue: the last < kWinBits bits, padded with ones; D3 tail rule
@@ -336,8 +333,7 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
     if (__builtin_amdgcn_ballot_w64(!fin))
     do
     {
-        const uint32_t hi = (uint32_t) (buf >> 32);
-        const uint32_t w = hi | (0xffffffffu >> (rem & 31));
+        const uint32_t w = W | (0xffffffffu >> (rem & 31));
         const uint32_t e = s_win[w >> (32 - kWinBits)];
         const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
         const bool two = (ns == 2) & (ct <= rem);
@@ -363,8 +359,13 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         const uint32_t nb = step ? (two ? 2u : 1u) : 0u;
         c = step ? c : 0;
         emit(val, nb);
-        buf <<= c;
         rem -= c;
+        const int32_t tn = (int32_t) t - (int32_t) c;
+        const bool cross = tn < 0;
+        A = cross ? B : A;
+        B = cross ? nx : B;
+        t = (uint32_t) tn & 31;
+        W = __builtin_amdgcn_alignbit(A, B, t);
         fin = fin | over | eos | (rem == 0);
     } while (__builtin_amdgcn_ballot_w64(!fin));
     emit.finish();
