@@ -652,6 +652,20 @@ up16(size_t x)
     return (x + 15) & ~(size_t) 15;
 }
 
+// The kernels' sticky error word, read from its pinned host mirror (the
+// kernels set both; call once the launch's stream has been synchronised):
+// no device round trip on the synchronous paths.
+static int
+mirror_error(qhuff_ctx *c)
+{
+    const uint32_t v = __atomic_exchange_n(&c->err_host[0], 0u, __ATOMIC_ACQ_REL);
+    if (!v)
+        return QHUFF_OK;
+    (void) hipMemset(c->err, 0, 4);
+    snprintf(c->err_msg, sizeof(c->err_msg), "device error %u", v);
+    return QHUFF_EDEVICE;
+}
+
 static int
 pipe_setup(qhuff_ctx *c)
 {
@@ -737,6 +751,9 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
     hipStream_t sk = c->own_stream;
     uint64_t base = 0;                           // output bytes so far
     uint32_t tot[kMaxChunks];
+    // a small batch brings its whole output bound back right behind the
+    // kernel: one synchronisation instead of two (latency, not bandwidth)
+    const bool small = K == 1 && ob[1] <= (4u << 20);
 
     auto stage_in = [&](unsigned i) -> int {
         const uint32_t s0 = cut[i], s1 = cut[i + 1];
@@ -765,6 +782,9 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
         if (!enc)
             HIPCHK(c, hipMemcpyAsync(H + o_st + s0, D + o_st + s0, s1 - s0,
                                      hipMemcpyDeviceToHost, sk));
+        if (small)
+            HIPCHK(c, hipMemcpyAsync(H + o_out, D + o_out, ob[1],
+                                     hipMemcpyDeviceToHost, sk));
         HIPCHK(c, hipEventRecord(c->ev_k[i], sk));
         return QHUFF_OK;
     };
@@ -772,6 +792,8 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
         HIPCHK(c, hipEventSynchronize(c->ev_k[i]));
         const uint32_t s1 = cut[i + 1];
         tot[i] = ((const uint32_t *) (H + o_oo))[s1 + i];
+        if (small)
+            return QHUFF_OK;                     // already here
         HIPCHK(c, hipStreamWaitEvent(c->d2h_stream, c->ev_k[i], 0));
         if (tot[i])
             HIPCHK(c, hipMemcpyAsync(H + o_out + ob[i], D + o_out + ob[i],
@@ -781,7 +803,8 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
         return QHUFF_OK;
     };
     auto unstage = [&](unsigned i) -> int {
-        HIPCHK(c, hipEventSynchronize(c->ev_out[i]));
+        if (!small)
+            HIPCHK(c, hipEventSynchronize(c->ev_out[i]));
         const uint32_t s0 = cut[i], s1 = cut[i + 1];
         c->pool->copy(out + base, H + o_out + ob[i], tot[i]);
         const uint32_t *ho = (const uint32_t *) (H + o_oo) + s0 + i;
@@ -819,15 +842,8 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
             return rc;
     out_off[n] = (uint32_t) base;
     {
-        uint32_t v = 0;
-        HIPCHK(c, hipMemcpy(&v, c->err, 4, hipMemcpyDeviceToHost));
-        c->err_host[0] = 0;              // (this check reports it)
-        if (v)
-        {
-            (void) hipMemset(c->err, 0, 4);
-            snprintf(c->err_msg, sizeof(c->err_msg), "device error %u", v);
-            return QHUFF_EDEVICE;
-        }
+        if ((rc = mirror_error(c)))
+            return rc;
     }
     return QHUFF_OK;
 }
@@ -912,25 +928,29 @@ qhuff_decode_literals_host(qhuff_ctx *c, const uint8_t *buf,
                                 c->d_stage + o_st, st);
         if (rc)
             return rc;
-        // sizes and status first (small), then exactly the decoded bytes
-        HIPCHK(c, hipMemcpyAsync(c->h_stage + o_oo, c->d_stage + o_oo,
-                                 4ull * (nh + 1), hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipMemcpyAsync(c->h_stage + o_st, c->d_stage + o_st, nh,
-                                 hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipStreamSynchronize(st));
-        const uint32_t dec_total = ((const uint32_t *) (c->h_stage + o_oo))[nh];
-        HIPCHK(c, hipMemcpyAsync(c->h_stage + o_out, c->d_stage + o_out,
-                                 dec_total, hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipStreamSynchronize(st));
-        uint32_t v = 0;
-        HIPCHK(c, hipMemcpy(&v, c->err, 4, hipMemcpyDeviceToHost));
-        c->err_host[0] = 0;              // (this check reports it)
-        if (v)
+        if (o_st + nh - o_out <= (4u << 20))
         {
-            (void) hipMemset(c->err, 0, 4);
-            snprintf(c->err_msg, sizeof(c->err_msg), "device error %u", v);
-            return QHUFF_EDEVICE;
+            // small: the decoded bytes' bound, sizes and status in one copy
+            HIPCHK(c, hipMemcpyAsync(c->h_stage + o_out, c->d_stage + o_out,
+                                     o_st + nh - o_out, hipMemcpyDeviceToHost,
+                                     st));
+            HIPCHK(c, hipStreamSynchronize(st));
         }
+        else
+        {
+            // sizes and status first, then exactly the decoded bytes
+            HIPCHK(c, hipMemcpyAsync(c->h_stage + o_oo, c->d_stage + o_oo,
+                                     4ull * (nh + 1), hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipMemcpyAsync(c->h_stage + o_st, c->d_stage + o_st, nh,
+                                     hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipStreamSynchronize(st));
+            const uint32_t dec_total = ((const uint32_t *) (c->h_stage + o_oo))[nh];
+            HIPCHK(c, hipMemcpyAsync(c->h_stage + o_out, c->d_stage + o_out,
+                                     dec_total, hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipStreamSynchronize(st));
+        }
+        if ((rc = mirror_error(c)))
+            return rc;
     }
     const uint32_t *doo = (const uint32_t *) (c->h_stage + o_oo);
     const uint8_t *dst = c->h_stage + o_st;
