@@ -503,9 +503,8 @@ coord(qhuff_ctx *c, uint64_t tiles)
 static uint32_t
 grid_for(uint64_t tiles, uint64_t waves_per_block, uint32_t cap)
 {
-    uint64_t need = (tiles + waves_per_block - 1) / waves_per_block;
-    if (need > kTickGroups)
-        need = (need + kTickGroups - 1) / kTickGroups * kTickGroups;
+    // (any number of workgroups: each covers every ticket group)
+    const uint64_t need = (tiles + waves_per_block - 1) / waves_per_block;
     return (uint32_t) (need < cap ? need : cap);
 }
 
