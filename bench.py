@@ -132,6 +132,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank; more ranks than GPUs (a rehearsal on a small box)
+    # share them round-robin
+    local = local % max(1, torch.cuda.device_count())
     if args.config4:
         return run_config4(args, np, torch, qhuff)
     if world > 1:
