@@ -632,16 +632,23 @@ struct TileOut
     {
         const uint32_t lane = lane_id();
         const uint32_t nfull = total >> 4, rem = total & 15;
+        // the lane's byte offset comes out of an opaque instruction here, at
+        // the store: left to itself the compiler hoists the 64-bit per-lane
+        // offset out of the tile loop and, at depth 3, spills it (a scratch
+        // reload and a vmcnt(0) before every flush)
+        uint32_t lo;
+        asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(lo) : "v"(lane));
         // (compile-time chunk index j throughout: a run-time select between
         // the o[] would put the array in scratch memory)
 #pragma unroll
         for (int j = 0; j < NCH; ++j)
         {
             const uint32_t k = lane + 64u * j;
+            uint8_t *p = dst + (lo + 1024u * j);
             if (k < nfull)
-                ((QH_GLB U4 *) (dst + 16u * k))->v = o[j];
+                ((QH_GLB U4 *) p)->v = o[j];
             else if (k == nfull && rem)
-                store_part(dst + 16u * k, o[j], rem);
+                store_part(p, o[j], rem);
         }
     }
     __device__ __forceinline__ static void store_part(uint8_t *dst, u32x4 v,
