@@ -413,23 +413,57 @@ struct GlobalEmit                            // slow path: byte stores
 };
 
 // arena slot -> stage at byte D (wave-synchronous; other lanes write the
-// neighbouring bytes): bytes up to a dword boundary, whole dwords, tail
+// neighbouring bytes).  Bytes up to D's dword boundary (head) and after the
+// last whole dword (tail) by byte stores, the whole dwords between from pairs
+// of aligned source words (alignbyte), four per trip with the reads of a trip
+// issued together: per trip one LDS round trip, not one per dword.
+__device__ __forceinline__ void
+write_bytes(QH_LDS uint8_t *d, uint32_t v, uint32_t nb)
+{
+    if (nb > 0)
+        d[0] = (uint8_t) v;
+    if (nb > 1)
+        d[1] = (uint8_t) (v >> 8);
+    if (nb > 2)
+        d[2] = (uint8_t) (v >> 16);
+}
+
 __device__ __forceinline__ void
 compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
 {
     uint32_t h = (4 - ((uint32_t) (uintptr_t) dstb & 3)) & 3;
     h = h < n ? h : n;
-    for (uint32_t i = 0; i < h; ++i)
-        dstb[i] = src[i];
-    const QH_LDS uint8_t *s2 = src + h;
-    const uint32_t s3 = (uint32_t) ((uintptr_t) s2 & 3);
-    const QH_LDS uint32_t *sw = (const QH_LDS uint32_t *) (s2 - s3);
-    QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
     const uint32_t nb = (n - h) >> 2;
-    for (uint32_t k = 0; k < nb; ++k)
-        dw[k] = align_bytes(sw[k + 1], sw[k], s3);
-    for (uint32_t i = h + 4 * nb; i < n; ++i)
-        dstb[i] = src[i];
+    const uint32_t nt = n - h - 4 * nb;
+    const uint32_t sa = (uint32_t) (uintptr_t) src;
+    const QH_LDS uint32_t *sw = (const QH_LDS uint32_t *) (src - (sa & 3));
+    const uint32_t s3 = sa & 3;
+    // head and tail: the 4 source bytes at src + i, i = 0 and h + 4 nb
+    const uint32_t it = h + 4 * nb;
+    const uint32_t qt = (s3 + it) >> 2;
+    const uint32_t vh = h ? align_bytes(sw[1], sw[0], s3) : 0u;
+    const uint32_t vt = nt ? align_bytes(sw[qt + 1], sw[qt], (s3 + it) & 3) : 0u;
+    write_bytes(dstb, vh, h);
+    write_bytes(dstb + it, vt, nt);
+    // body: source words from q0, shift r
+    const uint32_t sb = s3 + h, r = sb & 3;
+    const QH_LDS uint32_t *bw = sw + (sb >> 2);
+    QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
+    for (uint32_t k = 0; k < nb; k += 4)
+    {
+        const uint32_t w0 = bw[k];
+        const uint32_t w1 = bw[k + 1];
+        const uint32_t w2 = k + 1 < nb ? bw[k + 2] : 0u;
+        const uint32_t w3 = k + 2 < nb ? bw[k + 3] : 0u;
+        const uint32_t w4 = k + 3 < nb ? bw[k + 4] : 0u;
+        dw[k] = align_bytes(w1, w0, r);
+        if (k + 1 < nb)
+            dw[k + 1] = align_bytes(w2, w1, r);
+        if (k + 2 < nb)
+            dw[k + 2] = align_bytes(w3, w2, r);
+        if (k + 3 < nb)
+            dw[k + 3] = align_bytes(w4, w3, r);
+    }
 }
 
 // A tile whose input or output does not fit the stage, coded eagerly:
@@ -527,9 +561,13 @@ struct DecPolicy
         {
             const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
             const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
+#if QH_EXP == 1   // (timing experiment: no codec)
+            r = (int) (((re - rs) * 23) >> 4);
+#else
             ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
             r = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted,
                                   em);
+#endif
         }
         *sz = r < 0 ? 0u : (uint32_t) r;
         *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
@@ -537,7 +575,11 @@ struct DecPolicy
     // arena -> the (dead) input stage, compacted
     __device__ __forceinline__ void emit(uint32_t excl, uint32_t sz, uint32_t)
     {
+#if QH_EXP == 2   // (timing experiment: no compaction)
+        if (0)
+#else
         if (sz)
+#endif
             compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
                            sz);
     }

@@ -89,6 +89,10 @@ wait_vm_all()
     __builtin_amdgcn_s_waitcnt(0x0f70);
 }
 
+#ifndef QH_WAIT
+#define QH_WAIT 1
+#endif
+
 // The kernel prologue claims the first two tickets of every wave of the
 // workgroup: lanes 0..kTickGroups-1 of the first wave each take one group's
 // share with one returning atomic (~3,000 waves claiming one by one would
@@ -203,7 +207,8 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         prof_stamp(c, it, 0);
         // top: t's input, offsets and ticket (issued a codec ago), the last
         // iteration's stores and look-back start (an emit ago)
-        wait_vm_all();
+        if (QH_WAIT == 1 || QH_WAIT == 2)
+            wait_vm_all();
         prof_stamp(c, it, 1);
         // the newest pending tile's add has returned: publish the super
         // aggregate if it completed its super tile (as early as possible:
@@ -258,9 +263,16 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
             wave_sync();
         }
         prof_stamp(c, it, 9);
+#ifdef QHUFF_PROFILE
+        // (profiling only) split the wait: all but the youngest three -- the
+        // aggregate store and super add of lb.start, stamp 9 -- then the rest
+        __builtin_amdgcn_s_waitcnt(0x0f73);
+        prof_stamp(c, it, 10);
+#endif
 
         // the polls (a codec and an emit ago); resolve + store the oldest
-        wait_vm_all();
+        if (QH_WAIT == 1)
+            wait_vm_all();
         prof_stamp(c, it, 4);
         if (pend[0].valid)
             flush_tile<P::kStatus>(c, pend[0], outs[0], out, out_off, status,

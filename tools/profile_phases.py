@@ -4,7 +4,8 @@
 Slots per wave iteration (qhuff_pipeline.h): 0 top, 1 after the top wait,
 2 after stage + loads + polls, 3 after codec + scan, 9 after lb.start +
 emit, 4 after the poll wait, 7 after the older tile's look-back (inside the
-flush), 5 after the flush, 6 end of iteration (after the gather)."""
+flush), 5 after the flush, 6 end of iteration (after the gather); 10 (inside the poll wait) once all
+but lb.start's two operations have landed."""
 import os
 import sys
 
@@ -50,6 +51,13 @@ def report(tag, p):
         a = (p[:, :, 9] - p[:, :, 3])[ok]
         b = (p[:, :, 4] - p[:, :, 9])[ok]
         print("  start+emit mean %.0f p90 %.0f | poll wait mean %.0f p90 %.0f"
+              % (a.mean(), np.percentile(a, 90), b.mean(), np.percentile(b, 90)))
+    ok = live & (p[:, :, 9] != 0) & (p[:, :, 10] != 0) & (p[:, :, 4] != 0)
+    if ok.any():
+        a = (p[:, :, 10] - p[:, :, 9])[ok]
+        b = (p[:, :, 4] - p[:, :, 10])[ok]
+        print("  poll wait split: older ops mean %.0f p90 %.0f | own start "
+              "(aggregate store + super add) mean %.0f p90 %.0f"
               % (a.mean(), np.percentile(a, 90), b.mean(), np.percentile(b, 90)))
     if not os.environ.get("TIMELINE"):
         return
