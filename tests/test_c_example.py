@@ -41,6 +41,14 @@ def _build_hook_test():
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "c")])
 
 
+def _hook_test():
+    # built by __graft_entry__.build(); a GPU run from a tree that skipped it
+    # builds it here (gcc is on the box too)
+    if not os.path.exists(HOOK_TEST):
+        _build_hook_test()
+    return HOOK_TEST
+
+
 def test_hook_test_builds_and_links():
     """qhuff_hook.c compiles as gnu99 -Werror and links libqhuff.so (the
     test program also links the oracle, as the checker)."""
@@ -58,7 +66,7 @@ def test_hook_encoder_seam_matches_lsqpack_enc_enc_str():
     3/5/7, both dst[0] states and dst_len around the need (-1 included)."""
     files = [os.path.join(DATA, f + ".qif") for f in ("netbsd", "fb-req",
                                                       "fb-resp")]
-    r = subprocess.run([HOOK_TEST, "enc"] + files, capture_output=True,
+    r = subprocess.run([_hook_test(), "enc"] + files, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout and "misses 0" in r.stdout
@@ -72,7 +80,7 @@ def test_hook_decoder_seam_matches_lsqpack_huff_decode():
     n_src and bytes for dst_len around the decoded length."""
     files = [os.path.join(DATA, f + ".out.256.100.1")
              for f in ("netbsd", "fb-req", "fb-resp")]
-    r = subprocess.run([HOOK_TEST, "dec"] + files, capture_output=True,
+    r = subprocess.run([_hook_test(), "dec"] + files, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
