@@ -50,6 +50,15 @@ constexpr int kSuper = 64;                  // tiles per super tile
 // super-tile accumulator word: [63:48] tiles arrived, [47:0] byte sum
 constexpr uint64_t kAccOne = 1ull << 48;
 constexpr uint64_t kAccMask = kAccOne - 1;
+// accumulators kAccStride u64 apart (256 B, a line each): device-scope
+// atomics to one line are serialised (~88/us, MI355X_MICROARCH.md
+// 'dequeue'), and with 16 accumulators per line every running super tile's
+// adds queued on a handful of lines -- the returned add then cost ~3.5k
+// cycles of each tile's poll wait (profiles/r02_c/phases_*.txt)
+#ifndef QH_ACC_STRIDE
+#define QH_ACC_STRIDE 32
+#endif
+constexpr uint32_t kAccStride = QH_ACC_STRIDE;
 
 // error bits reported through Coord::err
 constexpr uint32_t kErrSpin = 1;            // look-back spin limit hit
@@ -74,7 +83,8 @@ struct Coord
     unsigned long long *prof;               // QHUFF_PROFILE builds: stamps
     unsigned long long *flags;              // per-tile look-back flags
     unsigned long long *sflags;             // per-super-tile flags
-    unsigned long long *sacc;               // super accumulators [2][cap_super]
+    unsigned long long *sacc;               // super accumulators [2][cap_super],
+                                            // kAccStride apart
     uint32_t *tick;                         // tile tickets [2][kTickGroups],
                                             // kTickStride apart
     uint32_t *err;                          // sticky device error word
@@ -219,7 +229,7 @@ clear_next_launch(const Coord &c)
     const uint32_t par = (c.epoch + 1) & 1;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < c.cap_super;
          i += gridDim.x * blockDim.x)
-        __hip_atomic_store(&c.sacc[(uint64_t) par * c.cap_super + i], 0ull,
+        __hip_atomic_store(&c.sacc[((uint64_t) par * c.cap_super + i) * kAccStride], 0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0 && threadIdx.x < kTickGroups)
         __hip_atomic_store(&c.tick[(par * kTickGroups + threadIdx.x) * kTickStride],
@@ -481,7 +491,7 @@ struct LookBack
             __hip_atomic_store(&c.flags[t], kFlagAgg | ep(c) | tot,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             acc_old = __hip_atomic_fetch_add(
-                &c.sacc[(uint64_t) (c.epoch & 1) * c.cap_super + s],
+                &c.sacc[((uint64_t) (c.epoch & 1) * c.cap_super + s) * kAccStride],
                 kAccOne + tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -529,6 +539,9 @@ struct LookBack
     // publishes its inclusive one
     __device__ __forceinline__ uint64_t finish(const Coord &c)
     {
+#if QH_EXP == 3   // (timing experiment: no look-back)
+        return 0;
+#endif
         const uint32_t lane = lane_id();
         const uint32_t f0 = s * kSuper;
         const uint32_t nq = tile - f0;               // earlier tiles in super

@@ -399,12 +399,12 @@ qhuff_decode_bound(uint64_t in_bytes, uint32_t n)
 
 // look-back workspace: the tile tickets [2][kTickGroups] (u32, kTickStride
 // apart), tile flags [cap_tiles], super flags [cap_super], super
-// accumulators [2][cap_super] (u64)
+// accumulators [2][cap_super] (u64, kAccStride apart)
 constexpr size_t kTickBytes = 4 * 2 * kTickGroups * kTickStride;
 static size_t
 lb_bytes(uint64_t cap_tiles, uint64_t cap_super)
 {
-    return kTickBytes + 8 * (cap_tiles + 3 * cap_super);
+    return kTickBytes + 8 * (cap_tiles + cap_super + 2 * cap_super * kAccStride);
 }
 
 // make room for the look-back workspace of `tiles` tiles and advance the

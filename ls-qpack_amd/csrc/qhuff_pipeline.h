@@ -52,6 +52,9 @@ struct Pending
     uint32_t tile, cnt, total;
     uint32_t excl;                   // this lane's tile-local output offset
     uint32_t stat;                   // this lane's status byte
+#if QH_EXP == 3
+    uint32_t fake_base;
+#endif
     LookBack lb;
 };
 
@@ -61,7 +64,11 @@ __device__ __forceinline__ void
 flush_tile(const Coord &c, Pending &d, const TileOut<kChunks> &o, uint8_t *out,
            uint32_t *out_off, uint8_t *status, uint64_t n, uint32_t it = ~0u)
 {
+#if QH_EXP == 3   // (timing experiment: no look-back; base = input offset)
+    const uint64_t base = d.fake_base;
+#else
     const uint64_t base = d.lb.finish(c);
+#endif
     prof_stamp(c, it, 7);
     prof_value(c, it, 8, d.lb.spins_seen);
     o.store(out + base, d.total);
@@ -91,6 +98,9 @@ wait_vm_all()
 
 #ifndef QH_WAIT
 #define QH_WAIT 1
+#endif
+#ifndef QH_EXP
+#define QH_EXP 0
 #endif
 
 // The kernel prologue claims the first two tickets of every wave of the
@@ -213,7 +223,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         // the newest pending tile's add has returned: publish the super
         // aggregate if it completed its super tile (as early as possible:
         // look-backs of later super tiles wait on it)
-        if (pend[D - 1].valid)
+        if (pend[D - 1].valid && QH_EXP != 3)
             pend[D - 1].lb.super_agg(c);
         if (sp_cur.staged)
             pol.stage_in(ch, sp_cur, o_cur);
@@ -227,7 +237,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         const uint32_t tz = clamp(tnn);
         o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
         kq = tnn < nt ? tk.claim(c) : kNone;
-        if (pend[0].valid)
+        if (pend[0].valid && QH_EXP != 3)
             pend[0].lb.poll(c);
         prof_stamp(c, it, 2);
 
@@ -257,7 +267,12 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
             cur.total = total;
             cur.excl = excl;
             cur.stat = st;
+#if QH_EXP == 3
+            cur.lb.tile = t;
+            cur.fake_base = o_cur.first();
+#else
             cur.lb.start(c, t, total);
+#endif
             wave_sync();
             pol.emit(excl, sz, total);
             wave_sync();
