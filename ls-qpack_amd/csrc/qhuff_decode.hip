@@ -29,6 +29,21 @@
 #ifndef QH_DEPTH
 #define QH_DEPTH 3
 #endif
+#ifndef QH_BORROW
+#define QH_BORROW 1
+#endif
+// bytes past the last slot's bound (the two-byte emitter writes one past
+// its end): 16 keeps a wave's region at 8,128 B, so 16 waves + the tables fit
+// the 160 KiB of LDS
+#ifndef QH_ARENA_SLACK
+#define QH_ARENA_SLACK 16
+#endif
+#ifndef QH_NXCOND
+#define QH_NXCOND 0
+#endif
+#ifndef QH_EMITCOND
+#define QH_EMITCOND 0
+#endif
 
 namespace qhuff {
 
@@ -51,7 +66,7 @@ static_assert(kDecInCap % 16 == 0 && kDecInCap <= kStageCap, "input cap");
 // byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
 // most 8/5 of its input, plus one byte written past the end by the
 // two-byte emitter
-constexpr int kArenaBytes = 2 * kWT + 8 * kDecInCap / 5 + 32;
+constexpr int kArenaBytes = 2 * kWT + 8 * kDecInCap / 5 + QH_ARENA_SLACK;
 
 struct DecWave                       // one wave's private LDS region
 {
@@ -317,13 +332,29 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         }
         emit(e, ns);
         rem -= c;
+#if QH_BORROW
+        // t - c borrows exactly when the window moves on a dword: one
+        // v_sub_co for both, the borrow (vcc) feeding the selects and p
+        uint32_t tn;
+        const bool cross = __builtin_sub_overflow(t, c, &tn);
+        A = cross ? B : A;
+        B = cross ? nx : B;
+        t = tn & 31;
+        p += cross ? 1u : 0u;
+#else
         const int32_t tn = (int32_t) t - (int32_t) c;
         const bool cross = tn < 0;
         A = cross ? B : A;
         B = cross ? nx : B;
         t = (uint32_t) tn & 31;
         p += cross ? 1u : 0u;
+#endif
+#if QH_NXCOND
+        if (cross)                           // exec-masked: crossing lanes only
+            nx = src[p];
+#else
         nx = src[p];
+#endif
         W = __builtin_amdgcn_alignbit(A, B, t);
         idx = rem >= kMain ? W >> (32 - kWinBits) : kHoldIdx;
     } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
@@ -383,8 +414,13 @@ struct ArenaEmit
     __device__ __forceinline__ void finish() { n = (uint32_t) (p - slot); }
     __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
     {
-        p[0] = (uint8_t) val;
-        p[1] = (uint8_t) (val >> 16);
+#if QH_EMITCOND
+        if (nb)                              // exec-masked: held lanes skip
+#endif
+        {
+            p[0] = (uint8_t) val;
+            p[1] = (uint8_t) (val >> 16);
+        }
         p += nb;
     }
 };

@@ -594,6 +594,12 @@ struct LookBack
                 break;
             fs = poll_super(c, back);
         }
+        // Every poll has been consumed, so nothing is outstanding here but
+        // the compiler cannot see that the re-poll loads (whose registers the
+        // flush reuses) have landed: without this wait it puts a vmcnt(0)
+        // into each partial-chunk store path of the flush, where it drains
+        // the tile's own dwordx4 stores issued just before (~2k cycles).
+        __builtin_amdgcn_s_waitcnt(0x0f70);
         if (lane == 0)
             __hip_atomic_store(&c.flags[tile],
                                kFlagInc | ep(c) | ((excl + total) & kValMask),
