@@ -38,6 +38,9 @@
 #ifndef QH_ARENA_SLACK
 #define QH_ARENA_SLACK 16
 #endif
+#ifndef QH_ADDR
+#define QH_ADDR 1
+#endif
 #ifndef QH_NXCOND
 #define QH_NXCOND 0
 #endif
@@ -309,14 +312,29 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
     // selects, behind a wave-uniform branch.
     constexpr uint32_t kMain = kWinBits;
     uint32_t W = __builtin_amdgcn_alignbit(A, B, t);
+#if QH_ADDR
+    // idx is the entry's byte offset: (W >> 17) & 0x7ffc for a live lane,
+    // the hold entry's for a held one -- one v_and_or on the step's chain
+    // (the two masks come off the rem compare, beside it)
+    auto win_addr = [](uint32_t w, bool live) -> uint32_t {
+        return ((w >> (32 - kWinBits - 2)) & (live ? 4u * (kWinSize - 1) : 0u))
+             | (live ? 0u : 4u * kHoldIdx);
+    };
+    uint32_t idx = win_addr(W, rem >= kMain);
+#else
     uint32_t idx = rem >= kMain ? W >> (32 - kWinBits) : kHoldIdx;
+#endif
     if (__builtin_amdgcn_ballot_w64(rem >= kMain))
     do
     {
+#if QH_ADDR
+        uint32_t e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
+#else
         uint32_t e = s_win[idx];
+#endif
         uint32_t c = ent_c(e);                // bits of the entry's symbols
         uint32_t ns = ent_ns(e);              // symbols (0: longer code)
-        if (__builtin_amdgcn_ballot_w64(e < (1u << 24)))
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(e < (1u << 24)) != 0, 0))
         {
             // a code of 14..30 bits; EOS, or a code running past the end,
             // rejects the string (D3)
@@ -356,7 +374,11 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         nx = src[p];
 #endif
         W = __builtin_amdgcn_alignbit(A, B, t);
+#if QH_ADDR
+        idx = win_addr(W, rem >= kMain);
+#else
         idx = rem >= kMain ? W >> (32 - kWinBits) : kHoldIdx;
+#endif
     } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
 
     // epilogue: the last < kWinBits bits, padded with ones; D3 tail rule

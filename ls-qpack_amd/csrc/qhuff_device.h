@@ -571,6 +571,8 @@ struct LookBack
             }
             ft = poll_tile(c);
         }
+        const uint32_t spins1 = spins;
+        uint32_t extra = 0;                          // windows past the two
         // 2. super tiles before this one, back to an inclusive one
         for (uint32_t back = 0; !done;)
         {
@@ -588,6 +590,7 @@ struct LookBack
                 ++back;
                 // the second window was polled with the first
                 fs = back == 1 ? fs1 : poll_super(c, back);
+                extra += back > 1 ? 1u : 0u;
                 continue;
             }
             if (!spin(c, &spins))
@@ -608,7 +611,7 @@ struct LookBack
                                 ? c.n_tiles - f0 : (uint32_t) kSuper;
         if (tile == f0 + in_super - 1)
             publish_super(c, kFlagInc, excl + total);
-        spins_seen = spins;
+        spins_seen = spins1 | ((spins - spins1) << 12) | (extra << 24);
         return excl;
     }
 };

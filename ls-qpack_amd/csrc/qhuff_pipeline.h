@@ -8,10 +8,8 @@
 // Per iteration, for tile t:
 //
 //   top    one wait for what the last iteration issued: t's input chunks and
-//          offsets and the ticket (a whole codec ago), the stores and the
-//          look-back start of the last iteration (an emit ago).  Publish the
-//          newer tile's super aggregate if its add completed the super tile.
-//          P::stage_in()
+//          offsets and the ticket (a whole codec ago), the stores of the last
+//          iteration.  P::stage_in()
 //          -- t's chunks into the LDS stage -- then the loads of the next
 //          tile's input, of the offsets of the tile after it and the next
 //          ticket, and the older pending tile's look-back polls: all of them
@@ -21,8 +19,10 @@
 //   scan   wave scan -> tile-local offsets, tile total; publish the tile
 //          aggregate and add it to the super accumulator (LookBack::start)
 //   emit   P::emit() -- compacted output of t into the LDS out stage
-//   flush  one wait (the polls, a codec and an emit ago); resolve the older
-//          pending tile's look-back and store its output (registers)
+//   flush  one wait (the polls, a codec and an emit ago, and t's super
+//          add); publish t's super tile's aggregate if t's add completed it;
+//          resolve the older pending tile's look-back and store its output
+//          (registers)
 //   gather t's output from the out stage into the freed registers (TileOut)
 //
 // P::kDepth tiles are pending at a time, all holding their output in
@@ -220,11 +220,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         if (QH_WAIT == 1 || QH_WAIT == 2)
             wait_vm_all();
         prof_stamp(c, it, 1);
-        // the newest pending tile's add has returned: publish the super
-        // aggregate if it completed its super tile (as early as possible:
-        // look-backs of later super tiles wait on it)
-        if (pend[D - 1].valid && QH_EXP != 3)
-            pend[D - 1].lb.super_agg(c);
         if (sp_cur.staged)
             pol.stage_in(ch, sp_cur, o_cur);
         wave_sync();
@@ -289,6 +284,12 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         if (QH_WAIT == 1)
             wait_vm_all();
         prof_stamp(c, it, 4);
+        // t's add has returned with the polls: publish its super tile's
+        // aggregate if that add completed it -- here, an emit after the add,
+        // not at the next iteration's top (look-backs of later super tiles
+        // wait on it: encode re-polled the super windows on 1 tile in 3)
+        if (cur.valid && QH_EXP != 3)
+            cur.lb.super_agg(c);
         if (pend[0].valid)
             flush_tile<P::kStatus>(c, pend[0], outs[0], out, out_off, status,
                                    n, it);
@@ -331,8 +332,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         sp_cur = sp_nxt;
     }
     wait_vm_all();
-    if (pend[D - 1].valid)
-        pend[D - 1].lb.super_agg(c);
 #pragma unroll
     for (int i = 0; i < D; ++i)
         if (pend[i].valid)

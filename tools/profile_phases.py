@@ -42,10 +42,15 @@ def report(tag, p):
     if ok.any():
         lbt = (p[:, :, 7] - p[:, :, 4])[ok]
         stt = (p[:, :, 5] - p[:, :, 7])[ok]
-        sp = p[:, :, 8][ok]
+        raw = p[:, :, 8][ok]
+        w1, w2, w3 = raw & 0xfff, (raw >> 12) & 0xfff, raw >> 24
+        sp = w1 + w2                            # re-polls of either window
         print("  flush: look-back mean %.0f p90 %.0f | stores mean %.0f | re-polls mean %.2f, >0 in %.1f%%, max %d"
               % (lbt.mean(), np.percentile(lbt, 90), stt.mean(), sp.mean(),
                  100.0 * (sp > 0).mean(), sp.max()))
+        print("  re-polls: tile window mean %.2f (>0 in %.1f%%) | super windows mean %.2f (>0 in %.1f%%) | windows past two mean %.2f (>0 in %.1f%%)"
+              % (w1.mean(), 100.0 * (w1 > 0).mean(), w2.mean(),
+                 100.0 * (w2 > 0).mean(), w3.mean(), 100.0 * (w3 > 0).mean()))
     ok = live & (p[:, :, 3] != 0) & (p[:, :, 9] != 0) & (p[:, :, 4] != 0)
     if ok.any():
         a = (p[:, :, 9] - p[:, :, 3])[ok]
