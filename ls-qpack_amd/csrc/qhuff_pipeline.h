@@ -99,6 +99,9 @@ wait_vm_all()
 #ifndef QH_WAIT
 #define QH_WAIT 1
 #endif
+#ifndef QH_TOPWAIT
+#define QH_TOPWAIT 1
+#endif
 #ifndef QH_EXP
 #define QH_EXP 0
 #endif
@@ -211,13 +214,23 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
 #pragma unroll
     for (int i = 0; i < D; ++i)
         pend[i].valid = false;
+    // the prologue's loads, drained here: every path into the loop top then
+    // has nothing outstanding that the top reads (see the top)
+    if (!QH_TOPWAIT)
+        wait_vm_all();
     uint32_t it = 0;
     for (;; ++it)
     {
         prof_stamp(c, it, 0);
-        // top: t's input, offsets and ticket (issued a codec ago), the last
-        // iteration's stores and look-back start (an emit ago)
-        if (QH_WAIT == 1 || QH_WAIT == 2)
+        // top: t's input, offsets and ticket were issued a codec ago and have
+        // landed at the last iteration's poll wait; what is still in flight
+        // here is that iteration's flush (stores, flag store, super publish),
+        // which nothing below reads.  The wait is kept (QH_TOPWAIT=1): without
+        // it (prologue loads drained before the loop instead) the per-tile
+        // top wait fell from 1.8k to 0.3k cycles but the kernels did not get
+        // faster (enc 65.6 / dec 68.7 vs 65.3 / 68.3 us, interleaved A/B,
+        // profiles/r02_g) -- the waves then wait longer in their look-backs.
+        if (QH_TOPWAIT)
             wait_vm_all();
         prof_stamp(c, it, 1);
         if (sp_cur.staged)
