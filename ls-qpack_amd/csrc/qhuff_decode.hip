@@ -591,6 +591,7 @@ struct DecPolicy
     static constexpr int kInCap = kDecInCap;
     static constexpr int kDepth = QH_DEPTH;       // pending tiles
     static constexpr int kOutCap = kStageCap;
+    static constexpr bool kPark = false;
     const uint8_t *in;
     QH_LDS DecSmem *sm;
     QH_LDS DecWave *wv;
@@ -605,6 +606,10 @@ struct DecPolicy
     __device__ __forceinline__ const QH_LDS uint32_t *out_stage() const
     {
         return wv->in;
+    }
+    __device__ __forceinline__ QH_LDS uint32_t *park_buf() const
+    {
+        return nullptr;
     }
     // staged tile: decode this lane's string into its arena slot
     __device__ __forceinline__ void codec(const TileOffs &to, uint32_t cnt,

@@ -59,6 +59,11 @@ constexpr uint64_t kAccMask = kAccOne - 1;
 #define QH_ACC_STRIDE 32
 #endif
 constexpr uint32_t kAccStride = QH_ACC_STRIDE;
+// tile flags kFlagStride u64 apart (1: dense, a poll window is 4 lines)
+#ifndef QH_FLAG_STRIDE
+#define QH_FLAG_STRIDE 1
+#endif
+constexpr uint32_t kFlagStride = QH_FLAG_STRIDE;
 
 // error bits reported through Coord::err
 constexpr uint32_t kErrSpin = 1;            // look-back spin limit hit
@@ -459,7 +464,7 @@ struct LookBack
         const uint32_t q = lane < nq ? lane : (nq ? nq - 1 : 0);
         // (the raw flag: finish() masks lanes past nq; no use of the loaded
         // value here, so the poll's latency is not waited for until then)
-        return __hip_atomic_load(&c.flags[nq ? tile - 1 - q : tile],
+        return __hip_atomic_load(&c.flags[(uint64_t) (nq ? tile - 1 - q : tile) * kFlagStride],
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // super flags s-1-lane-64*back, raw (see super_val)
@@ -488,7 +493,7 @@ struct LookBack
         acc_old = 0;
         if (lane_id() == 0)
         {
-            __hip_atomic_store(&c.flags[t], kFlagAgg | ep(c) | tot,
+            __hip_atomic_store(&c.flags[(uint64_t) t * kFlagStride], kFlagAgg | ep(c) | tot,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             acc_old = __hip_atomic_fetch_add(
                 &c.sacc[((uint64_t) (c.epoch & 1) * c.cap_super + s) * kAccStride],
@@ -604,7 +609,7 @@ struct LookBack
         // the tile's own dwordx4 stores issued just before (~2k cycles).
         __builtin_amdgcn_s_waitcnt(0x0f70);
         if (lane == 0)
-            __hip_atomic_store(&c.flags[tile],
+            __hip_atomic_store(&c.flags[(uint64_t) tile * kFlagStride],
                                kFlagInc | ep(c) | ((excl + total) & kValMask),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t in_super = c.n_tiles - f0 < (uint32_t) kSuper

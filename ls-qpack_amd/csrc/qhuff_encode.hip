@@ -31,8 +31,16 @@
 // (global reads / per-lane global writes).
 #include "qhuff_pipeline.h"
 
-#ifndef QH_DEPTH
-#define QH_DEPTH 2
+#ifndef QH_ENC_DEPTH
+#define QH_ENC_DEPTH 2
+#endif
+// QH_PARK=1: the oldest of the pending tiles waits in an LDS park buffer
+// instead of registers.  Measured with QH_ENC_DEPTH=3 (three tiles' outputs
+// in registers spill): look-back re-polls 0.7 -> 0.04 per tile, but 5 VGPRs
+// still spill in the dense pass and the park round trip costs -- enc 72.8 vs
+// 65.5 us at depth 2 (profiles/r02_h).  Off.
+#ifndef QH_PARK
+#define QH_PARK 0
 #endif
 
 namespace qhuff {
@@ -49,6 +57,9 @@ struct EncWave                                // one wave's private LDS region
     alignas(16) uint32_t dense[kDenseWords];    // codes back to back, MSB first
     alignas(16) uint32_t out[kEncOutCap / 4];   // byte code lengths until emit
     uint32_t s0[kSpanChunks];                   // dense offset of each chunk
+#if QH_PARK
+    alignas(16) uint32_t park[kStageCap / 4];   // oldest pending tile's output
+#endif
 };
 
 struct EncSmem
@@ -678,8 +689,9 @@ struct EncPolicy
 {
     static constexpr bool kStatus = false;
     static constexpr int kInCap = kEncInCap;
-    static constexpr int kDepth = QH_DEPTH;       // pending tiles
+    static constexpr int kDepth = QH_ENC_DEPTH;       // pending tiles
     static constexpr int kOutCap = kEncOutCap;
+    static constexpr bool kPark = QH_PARK;
     const uint8_t *in;
     uint32_t mode;                   // 0 payload, 3/5/7 literal prefix bits
     QH_LDS EncSmem *sm;
@@ -705,6 +717,17 @@ struct EncPolicy
     {
         return wv->out;
     }
+#if QH_PARK
+    __device__ __forceinline__ QH_LDS uint32_t *park_buf() const
+    {
+        return wv->park;
+    }
+#else
+    __device__ __forceinline__ QH_LDS uint32_t *park_buf() const
+    {
+        return nullptr;
+    }
+#endif
     // staged tile: size this lane's string (E1, and the E3 choice)
     __device__ __forceinline__ void codec(const TileOffs &to, uint32_t cnt,
                                           const Span &sp, uint32_t *sz,

@@ -404,7 +404,7 @@ constexpr size_t kTickBytes = 4 * 2 * kTickGroups * kTickStride;
 static size_t
 lb_bytes(uint64_t cap_tiles, uint64_t cap_super)
 {
-    return kTickBytes + 8 * (cap_tiles + cap_super + 2 * cap_super * kAccStride);
+    return kTickBytes + 8 * (cap_tiles * kFlagStride + cap_super + 2 * cap_super * kAccStride);
 }
 
 // make room for the look-back workspace of `tiles` tiles and advance the
@@ -486,7 +486,7 @@ coord(qhuff_ctx *c, uint64_t tiles)
 #endif
     k.tick = (uint32_t *) c->flags;
     k.flags = c->flags + kTickBytes / 8;
-    k.sflags = k.flags + c->cap_tiles;
+    k.sflags = k.flags + c->cap_tiles * kFlagStride;
     k.sacc = k.sflags + c->cap_super;
     k.cap_super = (uint32_t) c->cap_super;
     k.err = c->err;

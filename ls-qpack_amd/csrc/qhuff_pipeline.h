@@ -211,6 +211,19 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     constexpr int D = P::kDepth;
     Pending pend[D];
     TileOut<kChunks> outs[D];
+    // resolve + store pending tile i (compile-time i); with P::kPark the
+    // oldest one's output comes back from the park buffer first
+    auto flush_at = [&](int i, uint32_t itn) {
+        if (P::kPark && i == 0)
+        {
+            TileOut<kChunks> o;
+            o.gather(pol.park_buf());
+            flush_tile<P::kStatus>(c, pend[0], o, out, out_off, status, n, itn);
+        }
+        else
+            flush_tile<P::kStatus>(c, pend[i], outs[i], out, out_off, status,
+                                   n, itn);
+    };
 #pragma unroll
     for (int i = 0; i < D; ++i)
         pend[i].valid = false;
@@ -304,8 +317,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         if (cur.valid && QH_EXP != 3)
             cur.lb.super_agg(c);
         if (pend[0].valid)
-            flush_tile<P::kStatus>(c, pend[0], outs[0], out, out_off, status,
-                                   n, it);
+            flush_at(0, it);
 #pragma unroll
         for (int i = 0; i + 1 < D; ++i)
         {
@@ -313,6 +325,14 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
             outs[i] = outs[i + 1];
         }
         pend[D - 1] = cur;
+        // P::kPark: the oldest pending tile waits in the wave's LDS park
+        // buffer, not in registers (after the flush above has read the
+        // buffer: a wave's LDS operations execute in order)
+        if (P::kPark && pend[0].valid)
+        {
+            wave_sync();
+            outs[0].park(pol.park_buf());
+        }
         prof_stamp(c, it, 5);
 
         if (fast)
@@ -327,8 +347,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
                 if (pend[i].valid)
                 {
                     pend[i].lb.poll(c);
-                    flush_tile<P::kStatus>(c, pend[i], outs[i], out, out_off,
-                                           status, n);
+                    flush_at(i, ~0u);
                 }
             pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
                           status, n);
@@ -350,7 +369,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         if (pend[i].valid)
         {
             pend[i].lb.poll(c);
-            flush_tile<P::kStatus>(c, pend[i], outs[i], out, out_off, status, n);
+            flush_at(i, ~0u);
         }
 }
 
