@@ -657,6 +657,9 @@ struct TileOut
     // writes its whole dwords, then its last 0-3 bytes.
     __device__ __forceinline__ void store(uint8_t *dst, uint32_t total) const
     {
+#if QH_EXP == 4   // (timing experiment: 16-byte aligned stores, wrong bytes)
+        dst = (uint8_t *) ((uintptr_t) dst & ~(uintptr_t) 15);
+#endif
         const uint32_t lane = lane_id();
         const uint32_t nfull = total >> 4, rem = total & 15;
         // the lane's byte offset comes out of an opaque instruction here, at

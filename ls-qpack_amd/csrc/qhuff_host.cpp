@@ -296,6 +296,18 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
             if (k >= 1 && k <= (uint32_t) occ_d)
                 c->dec_grid = k * c->n_cu;
         }
+        // experiment: a percentage of the resident grid (half the CUs' worth
+        // of workgroups at 50: per-CU vs chip-wide limits)
+        const char *pc = getenv("QHUFF_GRID_PCT");
+        if (pc)
+        {
+            const uint32_t q = (uint32_t) strtoul(pc, nullptr, 0);
+            if (q >= 1 && q <= 100)
+            {
+                c->enc_grid = c->enc_grid * q / 100 ? c->enc_grid * q / 100 : 1;
+                c->dec_grid = c->dec_grid * q / 100 ? c->dec_grid * q / 100 : 1;
+            }
+        }
     }
     *ctx_out = c;
     return QHUFF_OK;

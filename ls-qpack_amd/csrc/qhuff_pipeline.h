@@ -235,6 +235,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     for (;; ++it)
     {
         prof_stamp(c, it, 0);
+        prof_realtime(c, it, 11);            // 100 MHz: the shader clock
         // top: t's input, offsets and ticket were issued a codec ago and have
         // landed at the last iteration's poll wait; what is still in flight
         // here is that iteration's flush (stores, flag store, super publish),

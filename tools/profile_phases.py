@@ -38,6 +38,30 @@ def report(tag, p):
             print("  %-12s mean %8.0f  p50 %8.0f  p90 %8.0f  max %8.0f cyc"
                   % (NAMES[ph], d.mean(), np.median(d), np.percentile(d, 90),
                      d.max()))
+    # shader clock: s_memtime cycles over s_memrealtime (100 MHz) ticks
+    # between a wave's first and last iteration starts
+    nit = live.sum(axis=1)
+    sel = nit >= 2
+    if sel.any():
+        rows = np.nonzero(sel)[0]
+        last = nit[sel] - 1
+        dm = p[rows, last, 0] - p[rows, 0, 0]
+        dr = p[rows, last, 11] - p[rows, 0, 11]
+        good = dr > 0
+        if good.any():
+            mhz = 100.0 * dm[good] / dr[good]
+            print("  shader clock  p10 %.0f  p50 %.0f  p90 %.0f MHz (s_memtime / s_memrealtime)"
+                  % (np.percentile(mhz, 10), np.median(mhz), np.percentile(mhz, 90)))
+    # wall-clock (100 MHz) of each wave's first iteration start and last
+    # iteration start, relative to the earliest wave: dispatch skew and span
+    r0 = p[live[:, 0], 0, 11]
+    if (r0 > 0).all() and len(r0):
+        base = r0.min()
+        st = (r0 - base) * 0.01
+        lastr = np.array([p[i, live[i].sum() - 1, 11] for i in np.nonzero(live[:, 0])[0]])
+        en = (lastr - base) * 0.01
+        print("  wave first-iteration start (us after the earliest): p50 %.2f  p90 %.2f  max %.2f;"
+              "  last-iteration start max %.2f us" % (np.median(st), np.percentile(st, 90), st.max(), en.max()))
     ok = live & (p[:, :, 4] != 0) & (p[:, :, 7] != 0)
     if ok.any():
         lbt = (p[:, :, 7] - p[:, :, 4])[ok]
