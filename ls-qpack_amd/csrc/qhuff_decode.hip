@@ -44,6 +44,17 @@
 #ifndef QH_NXCOND
 #define QH_NXCOND 0
 #endif
+// two main-loop steps per trip, one refill read per trip, dword emitter
+// (decode_string_lds).  Parity-green on MI355X but slower: codec 12.5k vs
+// 10.6k cycles per tile, dec 74.3 vs 68.3 us (profiles/r02_j) -- halving the
+// codec's LDS operations did not pay for ~35 % more VALU per step, so the
+// loop is not bound by LDS throughput.  Off.
+#ifndef QH_PAIR
+#define QH_PAIR 0
+#endif
+#if QH_PAIR && !QH_ADDR
+#error "QH_PAIR needs QH_ADDR"
+#endif
 #ifndef QH_EMITCOND
 #define QH_EMITCOND 0
 #endif
@@ -69,7 +80,13 @@ static_assert(kDecInCap % 16 == 0 && kDecInCap <= kStageCap, "input cap");
 // byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
 // most 8/5 of its input, plus one byte written past the end by the
 // two-byte emitter
+#if QH_PAIR
+// dword slot of string i: i + floor(2 * (rs_i - A) / 5) -- its output is at
+// most floor(8 len / 5) bytes, ceil(that / 4) <= floor(2 len / 5) + 1 dwords
+constexpr int kArenaBytes = 4 * (kWT + 2 * kDecInCap / 5 + 2);
+#else
 constexpr int kArenaBytes = 2 * kWT + 8 * kDecInCap / 5 + QH_ARENA_SLACK;
+#endif
 
 struct DecWave                       // one wave's private LDS region
 {
@@ -324,6 +341,70 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
 #else
     uint32_t idx = rem >= kMain ? W >> (32 - kWinBits) : kHoldIdx;
 #endif
+#if QH_PAIR
+    // Two steps per trip.  The refill read is issued once per trip: after a
+    // step of <= 13 bits that moved the window on a dword (t went from t0 to
+    // t0 - c + 32 >= 19), the next such step cannot move it again, so one
+    // prefetched dword serves both; a long code (<= 30 bits) re-reads it in
+    // its (wave-uniform) branch.  The symbol bytes of both steps are appended
+    // to the lane's dword accumulator together (Emit::put2): an aligned
+    // ds_write_b32 per four output bytes instead of two byte writes per step
+    // -- the codec's LDS cycles, not its VALU, bound it at 12 waves/CU.
+    auto lds_at = [&](uint32_t a) -> uint32_t {
+        return *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + a);
+    };
+    auto advance = [&](uint32_t c) {
+        uint32_t tn;
+        const bool cross = __builtin_sub_overflow(t, c, &tn);
+        A = cross ? B : A;
+        B = cross ? nx : B;
+        t = tn & 31;
+        p += cross ? 1u : 0u;
+    };
+    // long-code fix of a step whose entry e is a long-code marker (lanes
+    // with e >= 2^24 keep e, c, s)
+    auto long_fix = [&](uint32_t &e, uint32_t &c, uint32_t &sb) {
+        const bool lng = e < (1u << 24);
+        uint32_t L;
+        const uint32_t sym = long_code(W, s_sorted, &L);
+        const bool rej = lng & ((sym == 256) | (L > rem));
+        e = lng ? (rej ? 0u : sym) : e;
+        c = lng ? (rej ? 0u : L) : c;
+        sb = lng ? (rej ? 0u : 8u) : sb;
+        bad |= rej ? 1u : 0u;
+        rem = rej ? 0u : rem;
+    };
+    if (__builtin_amdgcn_ballot_w64(rem >= kMain))
+    do
+    {
+        uint32_t e1 = lds_at(idx);
+        uint32_t c1 = ent_c(e1);
+        uint32_t s1 = (e1 >> 21) & 0x18u;    // 8 * symbols
+        const bool lg1 = __builtin_amdgcn_ballot_w64(e1 < (1u << 24)) != 0;
+        if (__builtin_expect(lg1, 0))
+            long_fix(e1, c1, s1);
+        rem -= c1;
+        advance(c1);
+        W = __builtin_amdgcn_alignbit(A, B, t);
+        idx = win_addr(W, rem >= kMain);
+        if (__builtin_expect(lg1, 0))
+            nx = src[p];                     // a long step may have crossed
+        uint32_t e2 = lds_at(idx);
+        uint32_t c2 = ent_c(e2);
+        uint32_t s2 = (e2 >> 21) & 0x18u;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(e2 < (1u << 24)) != 0, 0))
+        {
+            nx = src[p];                     // step 1 may have crossed
+            long_fix(e2, c2, s2);
+        }
+        rem -= c2;
+        advance(c2);
+        nx = src[p];
+        W = __builtin_amdgcn_alignbit(A, B, t);
+        idx = win_addr(W, rem >= kMain);
+        emit.put2(e1, s1, e2, s2);
+    } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
+#else
     if (__builtin_amdgcn_ballot_w64(rem >= kMain))
     do
     {
@@ -380,6 +461,8 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         idx = rem >= kMain ? W >> (32 - kWinBits) : kHoldIdx;
 #endif
     } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
+
+#endif
 
     // epilogue: the last < kWinBits bits, padded with ones; D3 tail rule
     bool fin = bad || rem == 0;
@@ -444,6 +527,53 @@ struct ArenaEmit
             p[1] = (uint8_t) (val >> 16);
         }
         p += nb;
+    }
+};
+
+// dword emitter (QH_PAIR): output bytes gathered in a register and stored
+// as aligned dwords into the lane's dword-aligned arena slot; the bytes of a
+// step are the entry's sym0 [7:0] and sym1 [23:16] (sym1 = 0 in a
+// one-symbol entry, so two steps' bytes combine with one shift-or)
+struct DwordEmit
+{
+    QH_LDS uint32_t *slot;
+    uint32_t w;                      // dwords stored
+    uint32_t pend;                   // pending bytes, low pb bits
+    uint32_t pb;                     // pending bits: 0, 8, 16 or 24
+    uint32_t n;                      // output bytes (after finish())
+    __device__ __forceinline__ static uint32_t bytes(uint32_t e)
+    {
+        return __builtin_amdgcn_perm(e, e, 0x0c0c0200u);   // sym1 : sym0
+    }
+    // append the low nbits (0..32, a multiple of 8) of x, no bits above
+    __device__ __forceinline__ void put(uint32_t x, uint32_t nbits)
+    {
+        const uint32_t lo = pend | (x << pb);
+        const uint32_t hi = (x >> 1) >> (31 - pb);   // x >> (32 - pb); 0 at pb 0
+        const uint32_t tot = pb + nbits;
+        const bool full = tot >= 32;
+        if (full)
+            slot[w] = lo;
+        w += full ? 1u : 0u;
+        pend = full ? hi : lo;
+        pb = tot & 31;
+    }
+    __device__ __forceinline__ void put2(uint32_t e1, uint32_t s1, uint32_t e2,
+                                         uint32_t s2)
+    {
+        put(bytes(e1) | (bytes(e2) << s1), s1 + s2);
+    }
+    // nb (0..2) symbols of entry (or symbol) val
+    __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
+    {
+        const uint32_t b = __builtin_amdgcn_ubfe(bytes(val), 0, 8 * nb);
+        put(b, 8 * nb);
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if (pb)
+            slot[w] = pend;
+        n = 4 * w + pb / 8;
     }
 };
 
@@ -618,7 +748,11 @@ struct DecPolicy
     {
         const uint32_t lane = lane_id();
         const uint32_t A = to.first();
+#if QH_PAIR
+        slot0 = 4 * (lane + (uint32_t) ((2ull * (to.o0 - A)) / 5));
+#else
         slot0 = 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
+#endif
         int r = 0;
         if (lane < cnt)
         {
@@ -627,7 +761,11 @@ struct DecPolicy
 #if QH_EXP == 1   // (timing experiment: no codec)
             r = (int) (((re - rs) * 23) >> 4);
 #else
+#if QH_PAIR
+            DwordEmit em{(QH_LDS uint32_t *) (wv->arena + slot0), 0, 0, 0, 0};
+#else
             ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
+#endif
             r = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted,
                                   em);
 #endif
