@@ -52,6 +52,14 @@
 #ifndef QH_PAIR
 #define QH_PAIR 0
 #endif
+// long codes stall their lane and are decoded outside the step loop (no
+// long-code branch in the step)
+#ifndef QH_STALL
+#define QH_STALL 1
+#endif
+#if QH_STALL && !QH_ADDR
+#error "QH_STALL needs QH_ADDR"
+#endif
 #if QH_PAIR && !QH_ADDR
 #error "QH_PAIR needs QH_ADDR"
 #endif
@@ -404,6 +412,53 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         idx = win_addr(W, rem >= kMain);
         emit.put2(e1, s1, e2, s2);
     } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
+#elif QH_STALL
+    // A long-code marker entry (e < 2^24: c = ns = 0) stalls its lane where
+    // it is, like the hold entry.  The step loop runs while some lane with
+    // >= kMain bits left is not stalled -- so the step carries no long-code
+    // branch -- and the stalled lanes then take their long step together,
+    // outside the loop, and the loop resumes.
+    auto advance = [&](uint32_t c) {
+        uint32_t tn;
+        const bool cross = __builtin_sub_overflow(t, c, &tn);
+        A = cross ? B : A;
+        B = cross ? nx : B;
+        t = tn & 31;
+        p += cross ? 1u : 0u;
+    };
+    for (;;)
+    {
+        uint32_t e = kHoldEntry;
+        if (__builtin_amdgcn_ballot_w64(rem >= kMain))
+        do
+        {
+            e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
+            const uint32_t c = ent_c(e);
+            emit(e, ent_ns(e));
+            rem -= c;
+            advance(c);
+            nx = src[p];
+            W = __builtin_amdgcn_alignbit(A, B, t);
+            idx = win_addr(W, rem >= kMain);
+        } while (__builtin_amdgcn_ballot_w64((rem >= kMain) & (e >= (1u << 24))));
+        // lanes left with >= kMain bits sit on a code of 14..30 bits; EOS,
+        // or a code running past the end, rejects the string (D3)
+        if (__builtin_expect(!__builtin_amdgcn_ballot_w64(rem >= kMain), 1))
+            break;
+        const bool lng = rem >= kMain;
+        uint32_t L;
+        const uint32_t sym = long_code(W, s_sorted, &L);
+        const bool rej = lng & ((sym == 256) | (L > rem));
+        const bool ok = lng & !rej;
+        const uint32_t c = ok ? L : 0u;
+        emit(sym, ok ? 1u : 0u);
+        bad |= rej ? 1u : 0u;
+        rem = rej ? 0u : rem - c;
+        advance(c);
+        nx = src[p];
+        W = __builtin_amdgcn_alignbit(A, B, t);
+        idx = win_addr(W, rem >= kMain);
+    }
 #else
     if (__builtin_amdgcn_ballot_w64(rem >= kMain))
     do
