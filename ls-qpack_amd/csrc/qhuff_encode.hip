@@ -42,6 +42,11 @@
 #ifndef QH_PARK
 #define QH_PARK 0
 #endif
+// the dense pass's three stage rows read up front (one LDS round trip):
+// enc 66.1 vs 65.4 us, not kept (profiles/r02_l/ab_rows_first.txt)
+#ifndef QH_ROWS_FIRST
+#define QH_ROWS_FIRST 0
+#endif
 
 namespace qhuff {
 
@@ -482,6 +487,18 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
     wave_sync();
     QH_LDS u32x4 *lens4 = (QH_LDS u32x4 *) wv->out;
     uint32_t carry = 0, big = 0;
+#if QH_ROWS_FIRST
+    // the rows' stage chunks read together (one LDS round trip, not one per
+    // row behind the previous row's dense ORs)
+    u32x4 wrow[kChunks];
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k)
+    {
+        const uint32_t c = lane + 64u * k;
+        const uint32_t last = n16 ? n16 - 1 : 0;
+        wrow[k] = ((const QH_LDS u32x4 *) wv->in)[c < last ? c : last];
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < kChunks; ++k)
     {
@@ -489,8 +506,12 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
         // lets the rows' lookups overlap; chunks past the span read its last
         // staged chunk again, coded past its end and never read
         const uint32_t c = lane + 64u * k;
+#if QH_ROWS_FIRST
+        const u32x4 w = wrow[k];
+#else
         const uint32_t last = n16 ? n16 - 1 : 0;
         const u32x4 w = ((const QH_LDS u32x4 *) wv->in)[c < last ? c : last];
+#endif
         const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
         uint32_t m[16];
 #pragma unroll
