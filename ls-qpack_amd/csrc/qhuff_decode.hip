@@ -857,6 +857,7 @@ qhuff_decode_kernel(DecArgs a)
     __shared__ DecSmem smem;
     QH_LDS DecSmem *sm = (QH_LDS DecSmem *) &smem;
     const int tid = threadIdx.x;
+    prof_realtime(a.c, kProfIters - 1, 10);      // (profiling) wave entry
     Tickets tk;
     tk.init();
     {
@@ -890,6 +891,7 @@ qhuff_decode_kernel(DecArgs a)
         clear_next_launch(a.c);
     }
     __syncthreads();                 // the only workgroup barrier
+    prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
     DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
     uint32_t k0, k1;
     wave_tickets(tk, &sm->tk, &k0, &k1);

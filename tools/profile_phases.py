@@ -52,6 +52,16 @@ def report(tag, p):
             mhz = 100.0 * dm[good] / dr[good]
             print("  shader clock  p10 %.0f  p50 %.0f  p90 %.0f MHz (s_memtime / s_memrealtime)"
                   % (np.percentile(mhz, 10), np.median(mhz), np.percentile(mhz, 90)))
+    # (decode builds) wave entry and after-barrier wall clock, iteration 15
+    pe, pb_ = p[:, ITERS - 1, 10], p[:, ITERS - 1, 11]
+    sel2 = live[:, 0] & (pe > 0) & (pb_ > 0)
+    if sel2.any():
+        base = pe[sel2].min()
+        ent = (pe[sel2] - base) * 0.01
+        pro = (pb_[sel2] - pe[sel2]) * 0.01
+        fst = (p[sel2, 0, 11] - pb_[sel2]) * 0.01
+        print("  wave entry (us after the first): p50 %.2f max %.2f | prologue to barrier p50 %.2f max %.2f | barrier to first iteration p50 %.2f max %.2f"
+              % (np.median(ent), ent.max(), np.median(pro), pro.max(), np.median(fst), fst.max()))
     # wall-clock (100 MHz) of each wave's first iteration start and last
     # iteration start, relative to the earliest wave: dispatch skew and span
     r0 = p[live[:, 0], 0, 11]
