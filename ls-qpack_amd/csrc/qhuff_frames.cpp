@@ -23,7 +23,11 @@
 namespace {
 
 // lsqpack_dec_int (lsqpack.c:2372-2437) on a complete buffer: 0 ok, -1 the
-// buffer ends inside the integer, -2 the value does not fit 64 bits
+// buffer ends inside the integer, -2 the value does not fit 64 bits.  The
+// reference's other -2 (out of input after >= LSQPACK_UINT64_ENC_SZ = 11
+// bytes, lsqpack.c:2413-2423) counts bytes across resumed calls; in one call
+// the loop reads at most the prefix byte and 10 continuation bytes and
+// checks for input before the 10th, so out of input is always -1 here.
 int
 dec_int(const uint8_t **pp, const uint8_t *end, unsigned prefix_bits,
         uint64_t *v_out)
