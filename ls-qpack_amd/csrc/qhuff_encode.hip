@@ -44,6 +44,9 @@
 #endif
 // the dense pass's three stage rows read up front (one LDS round trip):
 // enc 66.1 vs 65.4 us, not kept (profiles/r02_l/ab_rows_first.txt)
+#ifndef QH_COPY4
+#define QH_COPY4 1
+#endif
 #ifndef QH_ROWS_FIRST
 #define QH_ROWS_FIRST 0
 #endif
@@ -610,6 +613,38 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
     // output word w0 + k (k >= 1) <- the window at dense bit s - od + 32 k
     const uint32_t x1 = s - od + 32, sh = x1 & 31;
     uint32_t q = x1 >> 5;
+#if QH_COPY4
+    // the words the string owns whole (w0 + 1 .. wl - 1) by plain stores,
+    // four per trip with the trip's reads issued together (one LDS round
+    // trip per four words, not one per word); the shared last word ORed
+    // after the loop, its two source words read before it
+    if (wl == w0)
+        return;
+    auto win = [&](uint32_t a, uint32_t b) -> uint32_t {
+        return sh ? __builtin_amdgcn_alignbit(a, b, 32 - sh) : a;
+    };
+    const uint32_t nmid = wl - w0 - 1;
+    const uint32_t la = dense[q + nmid], lb = dense[q + nmid + 1];
+    uint32_t cur = dense[q];
+    QH_LDS uint32_t *o = st + w0 + 1;
+    for (uint32_t k = 0; k < nmid; k += 4)
+    {
+        const uint32_t n1 = dense[q + k + 1];
+        const uint32_t n2 = dense[q + k + 2];
+        const uint32_t n3 = dense[q + k + 3];
+        const uint32_t n4 = dense[q + k + 4];
+        o[k] = bswap32(win(cur, n1));
+        if (k + 1 < nmid)
+            o[k + 1] = bswap32(win(n1, n2));
+        if (k + 2 < nmid)
+            o[k + 2] = bswap32(win(n2, n3));
+        if (k + 3 < nmid)
+            o[k + 3] = bswap32(win(n3, n4));
+        cur = n4;
+    }
+    __hip_atomic_fetch_or(&st[wl], bswap32(win(la, lb) & tailm),
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
     uint32_t cur = dense[q];
 #pragma unroll 2
     for (uint32_t w = w0 + 1; w <= wl; ++w)
@@ -624,6 +659,7 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
         cur = nxt;
         ++q;
     }
+#endif
 }
 
 // one string from the dense stream: framing, payload bits [s, s + bits),
