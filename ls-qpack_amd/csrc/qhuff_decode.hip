@@ -52,6 +52,9 @@
 #ifndef QH_PAIR
 #define QH_PAIR 0
 #endif
+#ifndef QH_COMPACT8
+#define QH_COMPACT8 1
+#endif
 // long codes stall their lane and are decoded outside the step loop (no
 // long-code branch in the step)
 #ifndef QH_STALL
@@ -692,6 +695,25 @@ compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
     const uint32_t sb = s3 + h, r = sb & 3;
     const QH_LDS uint32_t *bw = sw + (sb >> 2);
     QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
+#if QH_COMPACT8
+    // eight dwords per trip, the trip's source words read together and the
+    // last one carried into the next trip (reads past the string stay in
+    // the wave's LDS region or past the allocation, where LDS reads 0)
+    uint32_t cur = bw[0];
+    for (uint32_t k = 0; k < nb; k += 8)
+    {
+        uint32_t n[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            n[j] = bw[k + j + 1];
+        dw[k] = align_bytes(n[0], cur, r);
+#pragma unroll
+        for (int j = 1; j < 8; ++j)
+            if (k + j < nb)
+                dw[k + j] = align_bytes(n[j], n[j - 1], r);
+        cur = n[7];
+    }
+#else
     for (uint32_t k = 0; k < nb; k += 4)
     {
         const uint32_t w0 = bw[k];
@@ -707,6 +729,7 @@ compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
         if (k + 3 < nb)
             dw[k + 3] = align_bytes(w4, w3, r);
     }
+#endif
 }
 
 // A tile whose input or output does not fit the stage, coded eagerly:
