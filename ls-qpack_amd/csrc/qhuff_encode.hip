@@ -600,9 +600,27 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
     const uint32_t e = d + nb;
     const uint32_t w0 = d >> 5, wl = (e - 1) >> 5, od = d & 31;
     const uint32_t tailm = 0xffffffffu << (31 - ((e - 1) & 31));
+#if QH_COPY4
+    // Every read of the first word, the first trip and the last word is
+    // issued before any write (a wave's LDS operations run in order, so a
+    // read behind a write waits for it): a string of up to 6 output words
+    // costs one LDS round trip.  The words the string owns whole (w0 + 1 ..
+    // wl - 1) by plain stores, four per trip with the trip's reads issued
+    // together; its first and last words, shared with its neighbours and its
+    // framing / padding, by OR.
+    // output word w0 + k (k >= 1) <- the window at dense bit s - od + 32 k
+    const uint32_t q0 = s >> 5, os = s & 31;
+    const uint32_t x1 = s - od + 32, sh = x1 & 31, q = x1 >> 5;
+    const uint32_t nmid = wl > w0 ? wl - w0 - 1 : 0u;
+    auto win = [&](uint32_t a, uint32_t b) -> uint32_t {
+        return sh ? __builtin_amdgcn_alignbit(a, b, 32 - sh) : a;
+    };
+    const uint32_t a = dense[q0], b = dense[q0 + 1];
+    const uint32_t la = dense[q + nmid], lb = dense[q + nmid + 1];
+    uint32_t cur = dense[q];
+    uint32_t n1 = dense[q + 1], n2 = dense[q + 2], n3 = dense[q + 3],
+             n4 = dense[q + 4];
     {
-        const uint32_t q = s >> 5, os = s & 31;
-        const uint32_t a = dense[q], b = dense[q + 1];
         uint32_t v = os ? __builtin_amdgcn_alignbit(a, b, 32 - os) : a;
         v >>= od;
         if (w0 == wl)
@@ -610,29 +628,18 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
         __hip_atomic_fetch_or(&st[w0], bswap32(v), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // output word w0 + k (k >= 1) <- the window at dense bit s - od + 32 k
-    const uint32_t x1 = s - od + 32, sh = x1 & 31;
-    uint32_t q = x1 >> 5;
-#if QH_COPY4
-    // the words the string owns whole (w0 + 1 .. wl - 1) by plain stores,
-    // four per trip with the trip's reads issued together (one LDS round
-    // trip per four words, not one per word); the shared last word ORed
-    // after the loop, its two source words read before it
     if (wl == w0)
         return;
-    auto win = [&](uint32_t a, uint32_t b) -> uint32_t {
-        return sh ? __builtin_amdgcn_alignbit(a, b, 32 - sh) : a;
-    };
-    const uint32_t nmid = wl - w0 - 1;
-    const uint32_t la = dense[q + nmid], lb = dense[q + nmid + 1];
-    uint32_t cur = dense[q];
     QH_LDS uint32_t *o = st + w0 + 1;
     for (uint32_t k = 0; k < nmid; k += 4)
     {
-        const uint32_t n1 = dense[q + k + 1];
-        const uint32_t n2 = dense[q + k + 2];
-        const uint32_t n3 = dense[q + k + 3];
-        const uint32_t n4 = dense[q + k + 4];
+        if (k)
+        {
+            n1 = dense[q + k + 1];
+            n2 = dense[q + k + 2];
+            n3 = dense[q + k + 3];
+            n4 = dense[q + k + 4];
+        }
         o[k] = bswap32(win(cur, n1));
         if (k + 1 < nmid)
             o[k + 1] = bswap32(win(n1, n2));
@@ -645,6 +652,18 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
     __hip_atomic_fetch_or(&st[wl], bswap32(win(la, lb) & tailm),
                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #else
+    {
+        const uint32_t q = s >> 5, os = s & 31;
+        const uint32_t a = dense[q], b = dense[q + 1];
+        uint32_t v = os ? __builtin_amdgcn_alignbit(a, b, 32 - os) : a;
+        v >>= od;
+        if (w0 == wl)
+            v &= tailm;
+        __hip_atomic_fetch_or(&st[w0], bswap32(v), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    const uint32_t x1 = s - od + 32, sh = x1 & 31;
+    uint32_t q = x1 >> 5;
     uint32_t cur = dense[q];
 #pragma unroll 2
     for (uint32_t w = w0 + 1; w <= wl; ++w)
