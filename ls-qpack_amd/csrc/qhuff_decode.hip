@@ -52,6 +52,9 @@
 #ifndef QH_PAIR
 #define QH_PAIR 0
 #endif
+#ifndef QH_TAIL1
+#define QH_TAIL1 1
+#endif
 #ifndef QH_COMPACT8
 #define QH_COMPACT8 1
 #endif
@@ -522,6 +525,28 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
 
 #endif
 
+#if QH_TAIL1
+    // epilogue, one pass: the last < kWinBits (13) real bits hold at most
+    // two symbols (codes are >= 5 bits), both inside the window padded with
+    // ones, so one lookup decodes them; the bits after them cannot complete
+    // a code (its entry would have decoded it), so they are the padding, and
+    // the D3 tail rule (fewer than 8 bits, all ones) applies at once.  The
+    // EOS code (30 bits) cannot occur in 12 bits.
+    {
+        const bool live = !(bad || rem == 0);
+        const uint32_t w = W | (0xffffffffu >> (rem & 31));
+        const uint32_t e = s_win[w >> (32 - kWinBits)];
+        const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
+        const bool two = (ns == 2) & (ct <= rem);
+        const bool one = !two & (ns != 0) & (l0 <= rem);
+        const uint32_t c = two ? ct : (one ? l0 : 0u);
+        emit(e, live ? (two ? 2u : (one ? 1u : 0u)) : 0u);
+        const uint32_t r2 = rem - c;             // padding bits
+        const uint32_t inv = ~(w << (c & 31));   // padding bits at the top
+        const bool pad_ok = r2 < 8 && (r2 == 0 || (inv >> ((32 - r2) & 31)) == 0);
+        bad |= (live & !pad_ok) ? 1u : 0u;
+    }
+#else
     // epilogue: the last < kWinBits bits, padded with ones; D3 tail rule
     bool fin = bad || rem == 0;
     if (__builtin_amdgcn_ballot_w64(!fin))
@@ -562,6 +587,7 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         W = __builtin_amdgcn_alignbit(A, B, t);
         fin = fin | over | eos | (rem == 0);
     } while (__builtin_amdgcn_ballot_w64(!fin));
+#endif
     emit.finish();
     return bad ? -1 : (int) emit.n;
 }
