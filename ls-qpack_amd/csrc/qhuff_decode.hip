@@ -715,31 +715,42 @@ compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
     const uint32_t qt = (s3 + it) >> 2;
     const uint32_t vh = h ? align_bytes(sw[1], sw[0], s3) : 0u;
     const uint32_t vt = nt ? align_bytes(sw[qt + 1], sw[qt], (s3 + it) & 3) : 0u;
-    write_bytes(dstb, vh, h);
-    write_bytes(dstb + it, vt, nt);
     // body: source words from q0, shift r
     const uint32_t sb = s3 + h, r = sb & 3;
     const QH_LDS uint32_t *bw = sw + (sb >> 2);
     QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
 #if QH_COMPACT8
-    // eight dwords per trip, the trip's source words read together and the
+    // Eight dwords per trip, the trip's source words read together and the
     // last one carried into the next trip (reads past the string stay in
-    // the wave's LDS region or past the allocation, where LDS reads 0)
+    // the wave's LDS region or past the allocation, where LDS reads 0).
+    // The first trip's reads go out with the head's and tail's, before any
+    // write (the arena and the stage do not overlap; a wave's LDS operations
+    // run in order, so a read behind a write would wait for it).
     uint32_t cur = bw[0];
+    uint32_t nw[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        nw[j] = bw[j + 1];
+    write_bytes(dstb, vh, h);
+    write_bytes(dstb + it, vt, nt);
     for (uint32_t k = 0; k < nb; k += 8)
     {
-        uint32_t n[8];
+        if (k)
+        {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            n[j] = bw[k + j + 1];
-        dw[k] = align_bytes(n[0], cur, r);
+            for (int j = 0; j < 8; ++j)
+                nw[j] = bw[k + j + 1];
+        }
+        dw[k] = align_bytes(nw[0], cur, r);
 #pragma unroll
         for (int j = 1; j < 8; ++j)
             if (k + j < nb)
-                dw[k + j] = align_bytes(n[j], n[j - 1], r);
-        cur = n[7];
+                dw[k + j] = align_bytes(nw[j], nw[j - 1], r);
+        cur = nw[7];
     }
 #else
+    write_bytes(dstb, vh, h);
+    write_bytes(dstb + it, vt, nt);
     for (uint32_t k = 0; k < nb; k += 4)
     {
         const uint32_t w0 = bw[k];
