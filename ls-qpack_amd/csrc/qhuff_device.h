@@ -31,6 +31,12 @@ struct __attribute__((packed, aligned(1))) U1 { uint32_t v; };
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWT = 64;                     // strings per wave tile
+// tile offsets by one vector load + a DPP shift + a uniform load of the
+// entry after the tile: slower (enc 64.8 vs 63.4, dec 67.9 vs 66.7 us,
+// profiles/r02_o/ab_off1.txt); off
+#ifndef QH_OFF1
+#define QH_OFF1 0
+#endif
 #ifndef QH_WAVES
 #define QH_WAVES 12
 #endif
@@ -350,7 +356,16 @@ struct TileOffs
     {
         const uint32_t lane = lane_id();
         o0 = in_off[s0 + (lane < cnt ? lane : cnt)];
+#if QH_OFF1
+        // o1 is the next lane's o0 (one vector load, not two), lane 63's
+        // from a scalar load of the entry after the tile
+        const uint32_t last = in_off[s0 + cnt];
+        const uint32_t nx = (uint32_t) __builtin_amdgcn_update_dpp(
+            0, (int) o0, 0x130, 0xf, 0xf, false);   // wave_shl:1
+        o1 = lane == 63 ? last : nx;
+#else
         o1 = in_off[s0 + (lane + 1 < cnt ? lane + 1 : cnt)];
+#endif
     }
     __device__ __forceinline__ uint32_t first() const { return read_lane(o0, 0); }
     __device__ __forceinline__ uint32_t last() const { return read_lane(o1, 63); }
