@@ -138,8 +138,19 @@ def main():
     if args.config4:
         return run_config4(args, np, torch, qhuff)
     if world > 1:
-        # timing barrier + max-over-ranks only: host-side gloo, no RCCL
-        dist.init_process_group("gloo")
+        # timing barrier + max-over-ranks only: host-side gloo, no RCCL.
+        # Gloo announces its connections on stdout; rank 0's stdout carries
+        # only the JSON line, so its fd 1 points at stderr meanwhile.
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
