@@ -86,11 +86,24 @@ __device__ __forceinline__ uint32_t ent_sym1(uint32_t e) { return (e >> 16) & 0x
 // fit the LDS -- measured slower than 12 waves (dec 88 vs 86 us: the codec
 // is issue-bound and the look-backs wait longer), so the default is the
 // full 3,072 at 12 waves.
+// QH_DUAL: 128-string tiles, two strings per lane (2l and 2l + 1) decoded
+// as two interleaved chains, 6 chunks (6,144 B) of stage per wave, run at 8
+// waves per workgroup (the Makefile's dual build).
+#ifndef QH_DUAL
+#define QH_DUAL 0
+#endif
+#if QH_DUAL && QH_PAIR
+#error "QH_DUAL and QH_PAIR are exclusive"
+#endif
+constexpr bool kDual = QH_DUAL;
+constexpr int kDecNch = kDual ? 6 : kChunks;            // chunks per lane
+constexpr uint32_t kDecTS = kDual ? 2 * kWT : kWT;      // strings per tile
+constexpr int kDecStageCap = 64 * kDecNch * 16;
 #ifndef QH_DEC_IN_CAP
-#define QH_DEC_IN_CAP 3072
+#define QH_DEC_IN_CAP (QH_DUAL ? 5632 : 3072)
 #endif
 constexpr int kDecInCap = QH_DEC_IN_CAP;
-static_assert(kDecInCap % 16 == 0 && kDecInCap <= kStageCap, "input cap");
+static_assert(kDecInCap % 16 == 0 && kDecInCap <= kDecStageCap, "input cap");
 // byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
 // most 8/5 of its input, plus one byte written past the end by the
 // two-byte emitter
@@ -99,12 +112,12 @@ static_assert(kDecInCap % 16 == 0 && kDecInCap <= kStageCap, "input cap");
 // most floor(8 len / 5) bytes, ceil(that / 4) <= floor(2 len / 5) + 1 dwords
 constexpr int kArenaBytes = 4 * (kWT + 2 * kDecInCap / 5 + 2);
 #else
-constexpr int kArenaBytes = 2 * kWT + 8 * kDecInCap / 5 + QH_ARENA_SLACK;
+constexpr int kArenaBytes = 2 * kDecTS + 8 * kDecInCap / 5 + QH_ARENA_SLACK;
 #endif
 
 struct DecWave                       // one wave's private LDS region
 {
-    alignas(16) uint32_t in[kStageCap / 4];   // BE input dwords; output stage
+    alignas(16) uint32_t in[kDecStageCap / 4];   // BE input dwords; output stage
     alignas(16) uint8_t arena[kArenaBytes];
 };
 
@@ -592,6 +605,139 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
     return bad ? -1 : (int) emit.n;
 }
 
+// ---- QH_DUAL: two strings per lane ----------------------------------------
+
+// Lane l of a 128-string tile holds the offsets of strings 2l and 2l + 1 and
+// the end of 2l + 1 (indices clamped to the tile's count: lanes past it hold
+// empty strings at the tile end).
+struct TileOffs2
+{
+    uint32_t o0, o1, o2;
+
+    __device__ __forceinline__ void load(const QH_GLB uint32_t *in_off,
+                                         uint64_t s0, uint32_t cnt)
+    {
+        const uint32_t i0 = 2 * lane_id();
+        o0 = in_off[s0 + (i0 < cnt ? i0 : cnt)];
+        o1 = in_off[s0 + (i0 + 1 < cnt ? i0 + 1 : cnt)];
+        o2 = in_off[s0 + (i0 + 2 < cnt ? i0 + 2 : cnt)];
+    }
+    __device__ __forceinline__ uint32_t first() const { return read_lane(o0, 0); }
+    __device__ __forceinline__ uint32_t last() const { return read_lane(o2, 63); }
+};
+
+// One decode chain of decode_pair_lds: the state of decode_string_lds (the
+// A:B window at position t, the prefetched next dword, the window address)
+// and the lane's arena pointer.
+struct LdsChain
+{
+    uint32_t rem, A, B, t, p, nx, W, idx, bad;
+    QH_LDS uint8_t *slot, *q;
+
+    __device__ __forceinline__ static uint32_t win_addr(uint32_t w, bool live)
+    {
+        return ((w >> (32 - kWinBits - 2)) & (live ? 4u * (kWinSize - 1) : 0u))
+             | (live ? 0u : 4u * kHoldIdx);
+    }
+    __device__ __forceinline__ void init(const QH_LDS uint32_t *src,
+                                         uint32_t bit0, uint32_t bitend,
+                                         QH_LDS uint8_t *s)
+    {
+        rem = bitend - bit0;
+        const uint32_t i0 = bit0 >> 5, sk = bit0 & 31;
+        A = src[i0];
+        const uint32_t a1 = src[i0 + 1];
+        B = sk ? a1 : A;
+        t = (32 - sk) & 31;
+        p = sk ? i0 + 2 : i0 + 1;
+        nx = src[p];
+        bad = 0;
+        slot = q = s;
+        W = __builtin_amdgcn_alignbit(A, B, t);
+        idx = win_addr(W, rem >= kWinBits);
+    }
+    // the rest of a step whose window entry e has been read: the long-code
+    // fix behind a wave-uniform branch (EOS or a code running past the end
+    // rejects, D3), the arena bytes, the window moved on c bits
+    __device__ __forceinline__ void step(uint32_t e, const QH_LDS uint32_t *src,
+                                         const QH_LDS uint16_t *s_sorted)
+    {
+        uint32_t c = ent_c(e), ns = ent_ns(e);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(e < (1u << 24)) != 0, 0))
+        {
+            const bool lng = e < (1u << 24);
+            uint32_t L;
+            const uint32_t sym = long_code(W, s_sorted, &L);
+            const bool rej = lng & ((sym == 256) | (L > rem));
+            e = lng ? sym : e;
+            c = lng ? (rej ? 0u : L) : c;
+            ns = lng ? (rej ? 0u : 1u) : ns;
+            bad |= rej ? 1u : 0u;
+            rem = rej ? 0u : rem;
+        }
+        q[0] = (uint8_t) e;
+        q[1] = (uint8_t) (e >> 16);
+        q += ns;
+        rem -= c;
+        uint32_t tn;
+        const bool cross = __builtin_sub_overflow(t, c, &tn);
+        A = cross ? B : A;
+        B = cross ? nx : B;
+        t = tn & 31;
+        p += cross ? 1u : 0u;
+        nx = src[p];
+        W = __builtin_amdgcn_alignbit(A, B, t);
+        idx = win_addr(W, rem >= kWinBits);
+    }
+    // the last < kWinBits bits (decode_string_lds's one-pass epilogue)
+    __device__ __forceinline__ int tail(const QH_LDS uint32_t *s_win)
+    {
+        const bool live = !(bad || rem == 0);
+        const uint32_t w = W | (0xffffffffu >> (rem & 31));
+        const uint32_t e = s_win[w >> (32 - kWinBits)];
+        const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
+        const bool two = (ns == 2) & (ct <= rem);
+        const bool one = !two & (ns != 0) & (l0 <= rem);
+        const uint32_t c = two ? ct : (one ? l0 : 0u);
+        q[0] = (uint8_t) e;
+        q[1] = (uint8_t) (e >> 16);
+        q += live ? (two ? 2u : (one ? 1u : 0u)) : 0u;
+        const uint32_t r2 = rem - c;
+        const uint32_t inv = ~(w << (c & 31));
+        const bool pad_ok = r2 < 8 && (r2 == 0 || (inv >> ((32 - r2) & 31)) == 0);
+        bad |= (live & !pad_ok) ? 1u : 0u;
+        return bad ? -1 : (int) (q - slot);
+    }
+};
+
+// Two strings per lane, decoded together: both chains' window lookups are
+// issued before either is used, so the two dependent LDS round trips of a
+// step overlap (a chain with < kWinBits bits left reads the hold entry and
+// stands still).  The loop runs to the longer chain of the wave.
+__device__ __forceinline__ void
+decode_pair_lds(const QH_LDS uint32_t *src, uint32_t b0, uint32_t b1,
+                uint32_t b2, QH_LDS uint8_t *slot0, QH_LDS uint8_t *slot1,
+                const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
+                int *r0, int *r1)
+{
+    LdsChain x, y;
+    x.init(src, b0, b1, slot0);
+    y.init(src, b1, b2, slot1);
+    auto lds_at = [&](uint32_t a) -> uint32_t {
+        return *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + a);
+    };
+    if (__builtin_amdgcn_ballot_w64((x.rem >= kWinBits) | (y.rem >= kWinBits)))
+    do
+    {
+        const uint32_t ex = lds_at(x.idx);
+        const uint32_t ey = lds_at(y.idx);
+        x.step(ex, src, s_sorted);
+        y.step(ey, src, s_sorted);
+    } while (__builtin_amdgcn_ballot_w64((x.rem >= kWinBits) | (y.rem >= kWinBits)));
+    *r0 = x.tail(s_win);
+    *r1 = y.tail(s_win);
+}
+
 // byte-granular arena sink: two unconditional byte stores per step, the
 // entry's first symbol [7:0] and second [23:16] (ds_write_b8 / _d16_hi; the
 // second is overwritten by the next step when only one symbol was emitted)
@@ -829,21 +975,120 @@ dec_slow_tile(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
     }
 }
 
+#if QH_DUAL
+// dec_slow_tile for two strings per lane (strings 2l and 2l + 1)
+__device__ __noinline__ void
+dec_slow_tile2(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
+               uint32_t slot0, uint32_t slot1, uint32_t sz0, Coord c,
+               uint32_t t, uint32_t cnt, TileOffs2 to, Span sp, uint32_t sz,
+               uint32_t st, uint8_t *out, uint32_t *out_off, uint8_t *status,
+               uint64_t n)
+{
+    const uint32_t lane = lane_id();
+    const bool v0 = 2 * lane < cnt, v1 = 2 * lane + 1 < cnt;
+    const uint32_t r0s = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
+    const uint32_t r1s = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
+    const uint32_t r1e = (uint32_t) ((uintptr_t) (in + to.o2) - sp.pa);
+    const DecGlb src{(const QH_GLB uint32_t *) sp.pa};
+    uint32_t z0 = sz0, z1 = sz - sz0;
+    uint32_t st0 = st & 0xff, st1 = st >> 8;
+    if (!sp.staged)
+    {
+        int a = 0, b = 0;
+        if (v0)
+        {
+            CountEmit em{0};
+            a = decode_string(src, 8 * r0s, 8 * r1s, sm->win, sm->sorted, em);
+        }
+        if (v1)
+        {
+            CountEmit em{0};
+            b = decode_string(src, 8 * r1s, 8 * r1e, sm->win, sm->sorted, em);
+        }
+        z0 = a < 0 ? 0u : (uint32_t) a;
+        z1 = b < 0 ? 0u : (uint32_t) b;
+        st0 = a < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+        st1 = b < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+    }
+    const uint32_t incl = wave_incl_scan(z0 + z1);
+    const uint32_t excl = incl - (z0 + z1);
+    const uint32_t total = read_lane(incl, 63);
+    LookBack lb;
+    lb.start(c, t, total);
+    lb.super_agg(c);
+    lb.poll(c);
+    const uint64_t base = lb.finish(c);
+    uint8_t *d0 = out + base + excl;
+    uint8_t *d1 = d0 + z0;
+    if (sp.staged)
+    {
+        const QH_LDS uint8_t *a0 = wv->arena + slot0;
+        const QH_LDS uint8_t *a1 = wv->arena + slot1;
+        for (uint32_t i = 0; i < z0; ++i)
+            ((QH_GLB uint8_t *) d0)[i] = a0[i];
+        for (uint32_t i = 0; i < z1; ++i)
+            ((QH_GLB uint8_t *) d1)[i] = a1[i];
+    }
+    else
+    {
+        if (v0 && st0 == QHUFF_DEC_OK && z0)
+        {
+            GlobalEmit em{d0, 0};
+            decode_string(src, 8 * r0s, 8 * r1s, sm->win, sm->sorted, em);
+        }
+        if (v1 && st1 == QHUFF_DEC_OK && z1)
+        {
+            GlobalEmit em{d1, 0};
+            decode_string(src, 8 * r1s, 8 * r1e, sm->win, sm->sorted, em);
+        }
+    }
+    const uint64_t s0 = (uint64_t) t * kDecTS;
+    if (v0)
+    {
+        ((QH_GLB uint32_t *) out_off)[s0 + 2 * lane] = (uint32_t) (base + excl);
+        ((QH_GLB uint8_t *) status)[s0 + 2 * lane] = (uint8_t) st0;
+    }
+    if (v1)
+    {
+        ((QH_GLB uint32_t *) out_off)[s0 + 2 * lane + 1] =
+            (uint32_t) (base + excl + z0);
+        ((QH_GLB uint8_t *) status)[s0 + 2 * lane + 1] = (uint8_t) st1;
+    }
+    if (t == c.n_tiles - 1 && lane == 0)
+    {
+        ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + total);
+        if (base + total > 0xffffffffull)        // offsets are 32-bit
+            raise_error(c, kErrRange);
+    }
+}
+#endif
+
 // the decode side of the wave pipeline (qhuff_pipeline.h)
 struct DecPolicy
 {
     static constexpr bool kStatus = true;
     static constexpr int kInCap = kDecInCap;
     static constexpr int kDepth = QH_DEPTH;       // pending tiles
-    static constexpr int kOutCap = kStageCap;
+    static constexpr int kOutCap = kDecStageCap;
     static constexpr bool kPark = false;
+    static constexpr int kNch = kDecNch;          // 16-byte chunks per lane
+    static constexpr uint32_t kTS = kDecTS;       // strings per tile
+    static constexpr bool kPairs = kDual;         // two strings per lane
+#if QH_DUAL
+    using Offs = TileOffs2;
+#else
+    using Offs = TileOffs;
+#endif
     const uint8_t *in;
     QH_LDS DecSmem *sm;
     QH_LDS DecWave *wv;
     uint32_t slot0;                  // this lane's arena slot (current tile)
+    uint32_t slot1;                  // (QH_DUAL) its second string's
+    uint32_t sz0;                    // (QH_DUAL) its first string's size
 
-    __device__ __forceinline__ void stage_in(const Chunks<kChunks> &ch,
-                                             const Span &sp, const TileOffs &)
+    __device__ __forceinline__ uint32_t first_size() const { return sz0; }
+    __device__ __forceinline__ void stage_in(const Chunks<kNch> &ch,
+                                             const Span &sp, const Offs &)
     {
         ch.store<true>((QH_LDS u32x4 *) wv->in, sp.n16);
     }
@@ -857,11 +1102,28 @@ struct DecPolicy
         return nullptr;
     }
     // staged tile: decode this lane's string into its arena slot
-    __device__ __forceinline__ void codec(const TileOffs &to, uint32_t cnt,
+    __device__ __forceinline__ void codec(const Offs &to, uint32_t cnt,
                                           const Span &sp, uint32_t *sz,
                                           uint32_t *st)
     {
         const uint32_t lane = lane_id();
+#if QH_DUAL
+        // strings 2l and 2l + 1; lanes past the count decode empty strings
+        (void) cnt;
+        const uint32_t A = to.first();
+        slot0 = 4 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
+        slot1 = 4 * lane + 2 + (uint32_t) ((8ull * (to.o1 - A)) / 5);
+        const uint32_t b0 = 8 * (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
+        const uint32_t b1 = 8 * (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
+        const uint32_t b2 = 8 * (uint32_t) ((uintptr_t) (in + to.o2) - sp.pa);
+        int r0, r1;
+        decode_pair_lds(wv->in, b0, b1, b2, wv->arena + slot0,
+                        wv->arena + slot1, sm->win, sm->sorted, &r0, &r1);
+        sz0 = r0 < 0 ? 0u : (uint32_t) r0;
+        *sz = sz0 + (r1 < 0 ? 0u : (uint32_t) r1);
+        *st = (r0 < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK)
+            | (r1 < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK) << 8;
+#else
         const uint32_t A = to.first();
 #if QH_PAIR
         slot0 = 4 * (lane + (uint32_t) ((2ull * (to.o0 - A)) / 5));
@@ -887,10 +1149,19 @@ struct DecPolicy
         }
         *sz = r < 0 ? 0u : (uint32_t) r;
         *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+#endif
     }
     // arena -> the (dead) input stage, compacted
     __device__ __forceinline__ void emit(uint32_t excl, uint32_t sz, uint32_t)
     {
+#if QH_DUAL
+        if (sz0)
+            compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
+                           sz0);
+        if (sz - sz0)
+            compact_string(wv->arena + slot1,
+                           (QH_LDS uint8_t *) wv->in + excl + sz0, sz - sz0);
+#else
 #if QH_EXP == 2   // (timing experiment: no compaction)
         if (0)
 #else
@@ -898,16 +1169,22 @@ struct DecPolicy
 #endif
             compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
                            sz);
+#endif
     }
 
     __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
-                                              TileOffs to, Span sp, uint32_t sz,
+                                              Offs to, Span sp, uint32_t sz,
                                               uint32_t st, uint8_t *out,
                                               uint32_t *out_off, uint8_t *status,
                                               uint64_t n)
     {
+#if QH_DUAL
+        dec_slow_tile2(in, sm, wv, slot0, slot1, sp.staged ? sz0 : 0u, c, t,
+                       cnt, to, sp, sz, st, out, out_off, status, n);
+#else
         dec_slow_tile(in, sm, wv, slot0, c, t, cnt, to, sp, sz, st, out,
                       out_off, status, n);
+#endif
     }
 };
 
@@ -952,7 +1229,7 @@ qhuff_decode_kernel(DecArgs a)
     }
     __syncthreads();                 // the only workgroup barrier
     prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
-    DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
+    DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0, 0, 0};
     uint32_t k0, k1;
     wave_tickets(tk, &sm->tk, &k0, &k1);
     tile_pipeline(pol, a.c, tk, k0, k1, a.in, a.in_off,
@@ -979,6 +1256,12 @@ int
 decode_waves_per_block()
 {
     return kWaves;
+}
+
+uint32_t
+decode_tile_strings()
+{
+    return kDecTS;
 }
 
 size_t

@@ -768,6 +768,11 @@ struct EncPolicy
     static constexpr int kDepth = QH_ENC_DEPTH;       // pending tiles
     static constexpr int kOutCap = kEncOutCap;
     static constexpr bool kPark = QH_PARK;
+    static constexpr int kNch = kChunks;          // 16-byte chunks per lane
+    static constexpr uint32_t kTS = kWT;          // strings per tile
+    static constexpr bool kPairs = false;         // one string per lane
+    using Offs = TileOffs;
+    __device__ __forceinline__ uint32_t first_size() const { return 0; }
     const uint8_t *in;
     uint32_t mode;                   // 0 payload, 3/5/7 literal prefix bits
     QH_LDS EncSmem *sm;

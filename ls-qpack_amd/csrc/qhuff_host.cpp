@@ -569,7 +569,8 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
         HIPCHK(c, hipMemsetAsync(out_off, 0, 4, st));
         return QHUFF_OK;
     }
-    uint64_t tiles = (n + kWT - 1) / kWT;
+    const uint64_t ts = decode_tile_strings();
+    uint64_t tiles = (n + ts - 1) / ts;
     int rc = prepare_launch(c, tiles, st);
     if (rc)
         return rc;

@@ -78,5 +78,6 @@ size_t encode_lds_bytes();
 size_t decode_lds_bytes();
 int encode_waves_per_block();
 int decode_waves_per_block();
+uint32_t decode_tile_strings();            // strings per decode tile
 
 }  // namespace qhuff

@@ -51,7 +51,9 @@ struct Pending
     bool valid;
     uint32_t tile, cnt, total;
     uint32_t excl;                   // this lane's tile-local output offset
-    uint32_t stat;                   // this lane's status byte
+    uint32_t stat;                   // this lane's status byte (two strings
+                                     // per lane: [7:0], [15:8], and the
+                                     // first one's size [31:16])
 #if QH_EXP == 3
     uint32_t fake_base;
 #endif
@@ -59,9 +61,9 @@ struct Pending
 };
 
 // resolve a pending tile's base and store it from `o` (every lane)
-template <bool kStatus>
+template <class P>
 __device__ __forceinline__ void
-flush_tile(const Coord &c, Pending &d, const TileOut<kChunks> &o, uint8_t *out,
+flush_tile(const Coord &c, Pending &d, const TileOut<P::kNch> &o, uint8_t *out,
            uint32_t *out_off, uint8_t *status, uint64_t n, uint32_t it = ~0u)
 {
 #if QH_EXP == 3   // (timing experiment: no look-back; base = input offset)
@@ -73,11 +75,29 @@ flush_tile(const Coord &c, Pending &d, const TileOut<kChunks> &o, uint8_t *out,
     prof_value(c, it, 8, d.lb.spins_seen);
     o.store(out + base, d.total);
     const uint32_t lane = lane_id();
-    const uint64_t s0 = (uint64_t) d.tile * kWT;
-    if (lane < d.cnt)
+    const uint64_t s0 = (uint64_t) d.tile * P::kTS;
+    if (P::kPairs)
+    {
+        // lane l: strings 2l and 2l + 1 of the tile
+        const uint32_t i0 = 2 * lane;
+        if (i0 < d.cnt)
+        {
+            ((QH_GLB uint32_t *) out_off)[s0 + i0] = (uint32_t) (base + d.excl);
+            if (P::kStatus)
+                ((QH_GLB uint8_t *) status)[s0 + i0] = (uint8_t) d.stat;
+        }
+        if (i0 + 1 < d.cnt)
+        {
+            ((QH_GLB uint32_t *) out_off)[s0 + i0 + 1] =
+                (uint32_t) (base + d.excl + (d.stat >> 16));
+            if (P::kStatus)
+                ((QH_GLB uint8_t *) status)[s0 + i0 + 1] = (uint8_t) (d.stat >> 8);
+        }
+    }
+    else if (lane < d.cnt)
     {
         ((QH_GLB uint32_t *) out_off)[s0 + lane] = (uint32_t) (base + d.excl);
-        if (kStatus)
+        if (P::kStatus)
             ((QH_GLB uint8_t *) status)[s0 + lane] = (uint8_t) d.stat;
     }
     if (d.tile == c.n_tiles - 1 && lane == 0)
@@ -178,8 +198,9 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     uint32_t tn = tk.tile_of_u(k1);
     if (t >= nt)
         return;
+    constexpr uint32_t TS = P::kTS;          // strings per tile
     auto cnt_of = [&](uint32_t tt) -> uint32_t {
-        return (uint32_t) min((uint64_t) kWT, n - (uint64_t) tt * kWT);
+        return (uint32_t) min((uint64_t) TS, n - (uint64_t) tt * TS);
     };
     // the loads for tile ids past the end read the last tile instead
     // (fixed instruction counts; the data is never used)
@@ -189,16 +210,16 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
 
     // prologue: offsets of t and tn, input of t (landed at the top), the
     // ticket of the third iteration
-    TileOffs o_cur, o_nxt, o_nn;
-    o_cur.load(in_off, (uint64_t) t * kWT, cnt_of(t));
-    o_nxt.load(in_off, (uint64_t) clamp(tn) * kWT, cnt_of(clamp(tn)));
+    typename P::Offs o_cur, o_nxt, o_nn;
+    o_cur.load(in_off, (uint64_t) t * TS, cnt_of(t));
+    o_nxt.load(in_off, (uint64_t) clamp(tn) * TS, cnt_of(clamp(tn)));
     // a wave claims another tile only while its next one is real: a claimed
     // tile is always coded (tickets of a group are handed out in order, so
     // once tn is past the end every later claim is too)
     const uint32_t kNone = 0xffffffffu;
     uint32_t kq = tn < nt ? tk.claim(c) : kNone;
     Span sp_cur = tile_span(in, o_cur.first(), o_cur.last(), P::kInCap);
-    Chunks<kChunks> ch;
+    Chunks<P::kNch> ch;
     ch.load(sp_cur);
 
     // Tiles come from in-order tickets claimed two iterations ahead (one
@@ -210,19 +231,18 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     // registers).
     constexpr int D = P::kDepth;
     Pending pend[D];
-    TileOut<kChunks> outs[D];
+    TileOut<P::kNch> outs[D];
     // resolve + store pending tile i (compile-time i); with P::kPark the
     // oldest one's output comes back from the park buffer first
     auto flush_at = [&](int i, uint32_t itn) {
         if (P::kPark && i == 0)
         {
-            TileOut<kChunks> o;
+            TileOut<P::kNch> o;
             o.gather(pol.park_buf());
-            flush_tile<P::kStatus>(c, pend[0], o, out, out_off, status, n, itn);
+            flush_tile<P>(c, pend[0], o, out, out_off, status, n, itn);
         }
         else
-            flush_tile<P::kStatus>(c, pend[i], outs[i], out, out_off, status,
-                                   n, itn);
+            flush_tile<P>(c, pend[i], outs[i], out, out_off, status, n, itn);
     };
 #pragma unroll
     for (int i = 0; i < D; ++i)
@@ -257,7 +277,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), P::kInCap);
         ch.load(sp_nxt);
         const uint32_t tz = clamp(tnn);
-        o_nn.load(in_off, (uint64_t) tz * kWT, cnt_of(tz));
+        o_nn.load(in_off, (uint64_t) tz * TS, cnt_of(tz));
         kq = tnn < nt ? tk.claim(c) : kNone;
         if (pend[0].valid && QH_EXP != 3)
             pend[0].lb.poll(c);
@@ -289,6 +309,8 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
             cur.total = total;
             cur.excl = excl;
             cur.stat = st;
+            if constexpr (P::kPairs)
+                cur.stat = st | pol.first_size() << 16;
 #if QH_EXP == 3
             cur.lb.tile = t;
             cur.fake_base = o_cur.first();
