@@ -75,10 +75,26 @@
 
 namespace qhuff {
 
+// QH_NSBYTE: the LDS copy of the window table drops the entries' 32 - c
+// field ([31:26], masked off in the prologue), so the symbol count is the
+// whole top byte and the arena pointer advances by one SDWA add (byte 3 of
+// the entry as the operand) instead of a bfe + add.  The hold entry is then
+// 0 (c = 0, ns = 0): only the STALL loop may use it (it never tests a held
+// lane's entry for a long code).
+#ifndef QH_NSBYTE
+#define QH_NSBYTE 0
+#endif
+#if QH_NSBYTE && (!QH_STALL || QH_DUAL || QH_PAIR)
+#error "QH_NSBYTE needs the QH_STALL loop (not QH_DUAL / QH_PAIR)"
+#endif
+
 // window entry fields (qhuff_tables.h)
 __device__ __forceinline__ uint32_t ent_c(uint32_t e) { return (e >> 8) & 15; }
 __device__ __forceinline__ uint32_t ent_l0(uint32_t e) { return (e >> 12) & 15; }
-__device__ __forceinline__ uint32_t ent_ns(uint32_t e) { return (e >> 24) & 3; }
+__device__ __forceinline__ uint32_t ent_ns(uint32_t e)
+{
+    return QH_NSBYTE ? e >> 24 : (e >> 24) & 3;
+}
 __device__ __forceinline__ uint32_t ent_sym1(uint32_t e) { return (e >> 16) & 0xff; }
 
 // staged input bytes (the output stage, the dead input stage, always has the
@@ -123,7 +139,7 @@ struct DecWave                       // one wave's private LDS region
 
 // hold entry, one past the window table: c = 0, ns = 0, not a long code
 constexpr uint32_t kHoldIdx = kWinSize;
-constexpr uint32_t kHoldEntry = 1u << 26;
+constexpr uint32_t kHoldEntry = QH_NSBYTE ? 0u : 1u << 26;
 
 struct DecSmem
 {
@@ -197,6 +213,11 @@ main_step(bool act, uint32_t d, uint32_t &hi, uint32_t &lo, uint32_t &bits,
 {
     uint32_t e = s_win[hi >> (32 - kWinBits)];
     bool ok = true;
+#if QH_NSBYTE
+    // (the LDS entries carry no 32 - c field: bits consumed kept apart;
+    // cc = 32 for an empty step, as the field's 0 gave)
+    uint32_t cb = ent_c(e);
+#endif
     if (__builtin_amdgcn_ballot_w64((GATED ? act : true) & (e < (1u << 24))))
     {
         // a code of 13..30 bits: synthesize the entry of a one-symbol step
@@ -207,11 +228,20 @@ main_step(bool act, uint32_t d, uint32_t &hi, uint32_t &lo, uint32_t &bits,
         const uint32_t el = (sym & 0xff) | (L << 8) | (L << 12) | (1u << 24)
                           | ((32u - L) << 26);
         e = lng ? (ok ? el : 0u) : e;
+#if QH_NSBYTE
+        cb = lng ? (ok ? L : 0u) : cb;
+#endif
     }
     if (GATED)
         e = act ? e : 0u;
     const uint32_t nb = (e >> 24) & 3;       // 0 for a held lane
+#if QH_NSBYTE
+    if (GATED)
+        cb = act ? cb : 0u;
+    const uint32_t k = (32u - cb) & 31;      // 32 - bits consumed (0: none)
+#else
     const uint32_t k = e >> 26;              // 32 - bits consumed
+#endif
     const uint32_t cc = 32u - k;
     emit(e, nb);
     const uint32_t sh = __builtin_amdgcn_alignbit(hi, lo, k);
@@ -361,8 +391,16 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
     // the hold entry's for a held one -- one v_and_or on the step's chain
     // (the two masks come off the rem compare, beside it)
     auto win_addr = [](uint32_t w, bool live) -> uint32_t {
+#if QH_ADDR == 2
+        // one select after the masked shift: 3 VALU (lshr, and, cndmask)
+        // instead of 4 (two mask selects, lshr, and_or) -- the step is close
+        // to VALU-issue-bound, its dependency chain is one op longer
+        return live ? (w >> (32 - kWinBits - 2)) & (4u * (kWinSize - 1))
+                    : 4u * kHoldIdx;
+#else
         return ((w >> (32 - kWinBits - 2)) & (live ? 4u * (kWinSize - 1) : 0u))
              | (live ? 0u : 4u * kHoldIdx);
+#endif
     };
     uint32_t idx = win_addr(W, rem >= kMain);
 #else
@@ -1219,7 +1257,13 @@ qhuff_decode_kernel(DecArgs a)
         {
             const int i = tid + r * 64 * kWaves;
             if (i < kWinSize / 4)
+            {
+#if QH_NSBYTE
+                const uint32_t m = 0x03ffffffu;      // drop [31:26]
+                v[r] = (u32x4){v[r].x & m, v[r].y & m, v[r].z & m, v[r].w & m};
+#endif
                 sw[i] = v[r];
+            }
         }
         if (tid < 257)
             sm->sorted[tid] = so;
