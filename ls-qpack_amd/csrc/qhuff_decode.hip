@@ -58,6 +58,9 @@
 #ifndef QH_COMPACT8
 #define QH_COMPACT8 1
 #endif
+#ifndef QH_COMPACT64
+#define QH_COMPACT64 0
+#endif
 // long codes stall their lane and are decoded outside the step loop (no
 // long-code branch in the step)
 #ifndef QH_STALL
@@ -903,7 +906,48 @@ compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
     const uint32_t sb = s3 + h, r = sb & 3;
     const QH_LDS uint32_t *bw = sw + (sb >> 2);
     QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
-#if QH_COMPACT8
+#if QH_COMPACT64
+    // (experiment) the body as 8-byte stores: one dword first when the
+    // dword-aligned destination is not 8-aligned, then four ds_write_b64 per
+    // trip of eight source dwords read together (a 64-bit store moves 3
+    // dwords through the LDS port, two 32-bit stores 4), a last odd dword
+    const uint32_t a = (nb != 0) & ((((uint32_t) (uintptr_t) dw) & 4) != 0);
+    const uint32_t m = nb - a, nq = m >> 1;
+    const QH_LDS uint32_t *bq = bw + a;
+    QH_LDS uint32_t *dq = dw + a;            // 8-byte aligned
+    const uint32_t w0 = bw[0];
+    uint32_t cur = bq[0];
+    uint32_t nw[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        nw[j] = bq[j + 1];
+    write_bytes(dstb, vh, h);
+    write_bytes(dstb + it, vt, nt);
+    if (a)
+        dw[0] = align_bytes(cur, w0, r);
+    for (uint32_t k = 0; k < nq; k += 4)
+    {
+        if (k)
+        {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                nw[j] = bq[2 * k + j + 1];
+        }
+        uint32_t v[8];
+        v[0] = align_bytes(nw[0], cur, r);
+#pragma unroll
+        for (int j = 1; j < 8; ++j)
+            v[j] = align_bytes(nw[j], nw[j - 1], r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (k + j < nq)
+                *(QH_LDS uint64_t *) (dq + 2 * (k + j)) =
+                    (uint64_t) v[2 * j] | ((uint64_t) v[2 * j + 1] << 32);
+        cur = nw[7];
+    }
+    if (m & 1)
+        dq[2 * nq] = align_bytes(bq[2 * nq + 1], bq[2 * nq], r);
+#elif QH_COMPACT8
     // Eight dwords per trip, the trip's source words read together and the
     // last one carried into the next trip (reads past the string stay in
     // the wave's LDS region or past the allocation, where LDS reads 0).
