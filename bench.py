@@ -7,9 +7,11 @@ synthetic batch (config 2) + one decode pass over the Huffman payload of a
 1M-string batch (config 3), both through the C-ABI (libqhuff.so).  value =
 (raw bytes encoded + raw bytes decoded, summed over ranks) / wall time.
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU; strings are sharded, no
-collective on the data path: "scaling": "weak").
+Run: python bench.py [--gpus N --steps K --warmup W].  One process per GPU:
+under torch.distributed.run (WORLD_SIZE must equal --gpus), or, with no
+launcher, bench.py starts the N rank processes itself before anything touches
+the GPU (ranks beyond the visible GPUs share them round-robin).  Strings are
+sharded, no collective on the data path: "scaling": "weak".
 
 Input buffers are rotated over --copies device copies (default 4, > 512 MB
 footprint) so a step does not re-read the previous step's bytes from the
@@ -65,6 +67,8 @@ def parse():
                     default=True,
                     help="also time the PCIe-inclusive host-memory path "
                          "(rank 0; never `value`)")
+    ap.add_argument("--probe-launch", action="store_true",
+                    help=argparse.SUPPRESS)   # tests: ranks meet, no GPU
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
                                                   "pmc_latest.json"),
                     help="PMC traffic summary (tools/pmc_summary.py)")
@@ -122,8 +126,61 @@ def host_cpus():
             "smt": (logical // len(cores)) if cores else None}
 
 
+def free_port():
+    """An unused TCP port on 127.0.0.1 for the gloo rendezvous."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_check(gpus, env):
+    """--gpus against the launcher's WORLD_SIZE.  Returns None when bench.py
+    must start the ranks itself (no launcher, --gpus > 1), the world size
+    otherwise; raises SystemExit when the two disagree."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return None if gpus > 1 else 1
+    if int(ws) != gpus:
+        raise SystemExit("bench: WORLD_SIZE=%s but --gpus %d: one rank per "
+                         "GPU, the two must agree" % (ws, gpus))
+    return int(ws)
+
+
+def launch_plan(gpus, env, port):
+    """Environments of the --gpus ranks bench.py starts itself: the variables
+    torch.distributed.run would set (rendezvous on 127.0.0.1)."""
+    plan = []
+    for r in range(gpus):
+        e = dict(env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(gpus),
+                  "LOCAL_WORLD_SIZE": str(gpus), "GROUP_RANK": "0",
+                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        plan.append(e)
+    return plan
+
+
+def self_launch(gpus):
+    """`bench.py --gpus N` without an outside launcher: start N rank
+    processes (this process has not touched the GPU, and never does), wait
+    for them, exit with the worst status.  Rank 0 prints the JSON line."""
+    import subprocess
+    plan = launch_plan(gpus, os.environ, free_port())
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)]
+                              + sys.argv[1:], env=e) for e in plan]
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    sys.exit(bad[0] if bad else 0)
+
+
 def main():
     args = parse()
+    if args.config4:
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            sys.exit("bench: --config4 is one process driving --gpus devices "
+                     "(one host thread each); do not start it per rank")
+    elif rank_check(args.gpus, os.environ) is None:
+        return self_launch(args.gpus)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -151,6 +208,22 @@ def main():
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
+    if args.probe_launch:
+        # (tests/test_bench_launch.py) the rank plumbing alone, on the CPU:
+        # every rank reports its rank and planned device; rank 0 prints them
+        me = torch.tensor([rank, local], dtype=torch.int64)
+        got = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        if world > 1:
+            dist.all_gather(got, me)
+            dist.destroy_process_group()
+        else:
+            got = [me]
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "gpus_arg": args.gpus,
+                              "ranks": [int(g[0]) for g in got],
+                              "devices": [int(g[1]) for g in got]}),
+                  flush=True)
+        return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -429,9 +502,9 @@ def run_config4(args, np, torch, qhuff):
     """Config 4: one batch of --n4 strings over G GPUs of one process."""
     import threading
     G = args.gpus
-    if torch.cuda.device_count() < G:
-        sys.exit("config4: %d GPUs requested, %d visible"
-                 % (G, torch.cuda.device_count()))
+    # one device per shard; more shards than visible GPUs (a rehearsal on a
+    # small box) share them round-robin
+    ndev = max(1, torch.cuda.device_count())
     alpha = (qhuff.TOKEN_ALPHABET if args.alphabet == "token"
              else qhuff.BASE64_ALPHABET)
     N = args.n4
@@ -445,12 +518,12 @@ def run_config4(args, np, torch, qhuff):
 
     def worker(g):
         try:
-            torch.cuda.set_device(g)
-            dev = torch.device("cuda", g)
+            torch.cuda.set_device(g % ndev)
+            dev = torch.device("cuda", g % ndev)
             sd, soff, _ = S.shard_view(data, off, cuts, g)
             n = len(soff) - 1
             raw = int(soff[-1])
-            codec = qhuff.Codec(g)
+            codec = qhuff.Codec(g % ndev)
             st = torch.cuda.Stream(device=dev)
             with torch.cuda.stream(st):
                 d_in = [torch.from_numpy(np.ascontiguousarray(sd)).to(dev)
@@ -556,7 +629,7 @@ def run_config4(args, np, torch, qhuff):
                    "shard_raw_bytes": shard_bytes,
                    "shard_byte_balance": round(max(shard_bytes)
                                                / max(1, min(shard_bytes)), 6)},
-        "per_gpu": [{"gpu": g, "wall_ms": round(r["wall"] * 1e3, 3),
+        "per_gpu": [{"gpu": g, "device": g % ndev, "wall_ms": round(r["wall"] * 1e3, 3),
                      "gbps": round(2 * r["raw"] * args.steps / r["wall"]
                                    / 1e9, 3)} for g, r in enumerate(res)],
         "stitched_equals_single_pass": bool(stitched_ok),
