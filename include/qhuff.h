@@ -36,7 +36,12 @@
 extern "C" {
 #endif
 
-#define QHUFF_ABI_VERSION 1
+/* 2: qhuff_huff_decode_ex (the reference's full argument list) added beside
+ * the 5-argument qhuff_huff_decode of version 1, which is unchanged */
+#define QHUFF_ABI_VERSION 2
+
+/* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
+int qhuff_abi_version(void);
 
 /* return codes */
 #define QHUFF_OK          0
@@ -166,9 +171,16 @@ struct qhuff_huff_decode_state
  * qhuff_lsqpack_set_decode_full (qhuff_lsqpack.h, which documents the exact
  * semantics). */
 struct qhuff_decode_retval
+qhuff_huff_decode_ex(qhuff_ctx *ctx, const unsigned char *src, int src_len,
+                     unsigned char *dst, int dst_len,
+                     struct qhuff_huff_decode_state *state, int final);
+
+/* (ABI 1) a complete string: qhuff_huff_decode_ex with a zeroed state and
+ * final = 1 -- OK, ERROR with n_dst = n_src = 0, or END_DST with the
+ * reference's partial progress when dst_len is too small */
+struct qhuff_decode_retval
 qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, int src_len,
-                  unsigned char *dst, int dst_len,
-                  struct qhuff_huff_decode_state *state, int final);
+                  unsigned char *dst, int dst_len);
 
 /* ---- literal-span pre-parse + batched literal decode (SURVEY.md 8(f)
  * rank 3).  A host pass walks only the instruction framing of QPACK wire

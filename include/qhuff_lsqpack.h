@@ -52,7 +52,7 @@ int qhuff_lsqpack_enc_enc_str(unsigned prefix_bits, unsigned char *dst,
  *   otherwise (resumed or non-final chunks: streaming input): the registered
  *   streaming decoder (the reference's own lsqpack_huff_decode_full,
  *   lsqpack.c:3443, always exported); with none registered: ERROR.
- * (qhuff_huff_decode in qhuff.h is the same on an explicit context.)
+ * (qhuff_huff_decode_ex in qhuff.h is the same on an explicit context.)
  * One deviation: an invalid string whose output overflows dst before the
  * point where the reference detects the error returns ERROR where the
  * reference returns END_DST first (the caller's retry reaches the ERROR). */

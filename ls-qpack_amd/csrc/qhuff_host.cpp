@@ -1081,7 +1081,7 @@ qhuff_enc_str_size(qhuff_ctx *c, const unsigned char *str, unsigned str_len)
     return rc == QHUFF_OK ? oo[1] : 0;
 }
 
-// qhuff_huff_decode (lsqpack_huff_decode with its full signature): see
+// qhuff_huff_decode_ex (lsqpack_huff_decode with its full signature): see
 // qhuff_shim.cpp
 
 // ---- host helpers --------------------------------------------------------------

@@ -133,8 +133,14 @@ wait_vm_all()
 // in the workgroup gets tickets base + r and base + n_g + r (n_g waves of
 // the workgroup in group g).  The second tickets only when the grid's first
 // claims cannot cover every tile (a small batch then gets one tile per wave,
-// not two per wave of the first workgroups to start); otherwise a sentinel
-// ticket whose tile lies past any batch.
+// not two per wave of the first workgroups to start); otherwise kClaimNow:
+// the wave claims its second ticket itself once it runs, like every later
+// one (a second tile fixed to whichever workgroup claimed it would need the
+// whole grid resident: with only some workgroups resident, e.g. beside
+// another context, a group's tickets could run ahead of another's and the
+// look-backs above the gap wait for tiles no running wave can claim).
+constexpr uint32_t kClaimNow = 0xffffffffu;   // second ticket: claim it in
+                                              // the wave (tile_pipeline)
 struct BlockTickets
 {
     uint32_t base[kTickGroups];
@@ -180,8 +186,7 @@ wave_tickets(const Tickets &tk, const QH_LDS BlockTickets *bt, uint32_t *k0,
     const uint32_t r = (threadIdx.x >> 6) / kTickGroups;
     const uint32_t nq = tick_group_waves(tk.g);
     *k0 = bt->base[tk.g] + r;
-    *k1 = bt->two ? bt->base[tk.g] + nq + r
-                  : 0xffffffffu / kTickGroups - kWaves;   // tile past the end
+    *k1 = bt->two ? bt->base[tk.g] + nq + r : kClaimNow;
 }
 
 template <class P>
@@ -195,7 +200,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     // tiles of this wave's first two iterations (tickets k0 < k1, claimed
     // for the whole block in the kernel prologue)
     uint32_t t = tk.tile_of_u(k0);
-    uint32_t tn = tk.tile_of_u(k1);
     if (t >= nt)
         return;
     constexpr uint32_t TS = P::kTS;          // strings per tile
@@ -212,6 +216,8 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     // ticket of the third iteration
     typename P::Offs o_cur, o_nxt, o_nn;
     o_cur.load(in_off, (uint64_t) t * TS, cnt_of(t));
+    // (wave-uniform; small batches only: one returning atomic, waited for)
+    uint32_t tn = k1 == kClaimNow ? tk.tile_of(tk.claim(c)) : tk.tile_of_u(k1);
     o_nxt.load(in_off, (uint64_t) clamp(tn) * TS, cnt_of(clamp(tn)));
     // a wave claims another tile only while its next one is real: a claimed
     // tile is always coded (tickets of a group are handed out in order, so

@@ -1,6 +1,6 @@
 // qhuff_shim.cpp -- the reference's per-string entry points with their exact
 // argument lists (include/qhuff_lsqpack.h) and the context form of
-// lsqpack_huff_decode (include/qhuff.h qhuff_huff_decode).
+// lsqpack_huff_decode (include/qhuff.h qhuff_huff_decode_ex).
 //
 // A complete string is decoded on the GPU (a one-string batch).  When the
 // caller's dst is too small, or the string holds a code longer than 16 bits,
@@ -68,9 +68,9 @@ constexpr qhuff_decode_retval kErr = {QHUFF_HUFF_DEC_ERROR, 0, 0};
 }  // namespace
 
 extern "C" struct qhuff_decode_retval
-qhuff_huff_decode(qhuff_ctx *c, const unsigned char *src, int src_len,
-                  unsigned char *dst, int dst_len,
-                  struct qhuff_huff_decode_state *state, int final)
+qhuff_huff_decode_ex(qhuff_ctx *c, const unsigned char *src, int src_len,
+                     unsigned char *dst, int dst_len,
+                     struct qhuff_huff_decode_state *state, int final)
 {
     if (!c || !state || src_len < 0 || dst_len < 0 || (!src && src_len)
             || (!dst && dst_len))
@@ -143,6 +143,20 @@ qhuff_lsqpack_enc_enc_str(unsigned prefix_bits, unsigned char *dst,
 }
 
 extern "C" struct qhuff_decode_retval
+qhuff_huff_decode(qhuff_ctx *c, const unsigned char *src, int src_len,
+                  unsigned char *dst, int dst_len)
+{
+    struct qhuff_huff_decode_state st = {0, {0, 0}};
+    return qhuff_huff_decode_ex(c, src, src_len, dst, dst_len, &st, 1);
+}
+
+extern "C" int
+qhuff_abi_version(void)
+{
+    return QHUFF_ABI_VERSION;
+}
+
+extern "C" struct qhuff_decode_retval
 qhuff_lsqpack_huff_decode(const unsigned char *src, int src_len,
                           unsigned char *dst, int dst_len,
                           struct qhuff_huff_decode_state *state, int final)
@@ -154,7 +168,7 @@ qhuff_lsqpack_huff_decode(const unsigned char *src, int src_len,
         return full ? full(src, src_len, dst, dst_len, state, final) : kErr;
     }
     qhuff_ctx *c = default_ctx();
-    return c ? qhuff_huff_decode(c, src, src_len, dst, dst_len, state, final)
+    return c ? qhuff_huff_decode_ex(c, src, src_len, dst, dst_len, state, final)
              : kErr;
 }
 

@@ -26,7 +26,8 @@ EXPORTS = (
     "qhuff_open", "qhuff_close", "qhuff_encode_bound", "qhuff_decode_bound",
     "qhuff_encode_batch", "qhuff_decode_batch", "qhuff_encode_batch_host",
     "qhuff_decode_batch_host", "qhuff_enc_enc_str", "qhuff_enc_str_size",
-    "qhuff_huff_decode", "qhuff_last_error", "qhuff_shard_cuts",
+    "qhuff_huff_decode", "qhuff_huff_decode_ex", "qhuff_abi_version",
+    "qhuff_last_error", "qhuff_shard_cuts",
     "qhuff_synth_batch", "qhuff_device_error", "qhuff_profile_read",
     "qhuff_xxh32_headers", "qhuff_xxh32_batch",
     "qhuff_scan_field_section", "qhuff_scan_encoder_stream",
@@ -117,9 +118,13 @@ def lib():
         L.qhuff_profile_read.argtypes = [vp, vp, C.c_uint64]
         L.qhuff_enc_str_size.restype = C.c_uint
         L.qhuff_enc_str_size.argtypes = [vp, C.c_char_p, C.c_uint]
+        L.qhuff_huff_decode_ex.restype = DecodeRetval
+        L.qhuff_huff_decode_ex.argtypes = [vp, vp, C.c_int, vp, C.c_int,
+                                           C.POINTER(DecodeState), C.c_int]
         L.qhuff_huff_decode.restype = DecodeRetval
-        L.qhuff_huff_decode.argtypes = [vp, vp, C.c_int, vp, C.c_int,
-                                        C.POINTER(DecodeState), C.c_int]
+        L.qhuff_huff_decode.argtypes = [vp, vp, C.c_int, vp, C.c_int]
+        L.qhuff_abi_version.restype = C.c_int
+        L.qhuff_abi_version.argtypes = []
         L.qhuff_lsqpack_enc_enc_str.restype = C.c_int
         L.qhuff_lsqpack_enc_enc_str.argtypes = [C.c_uint, vp, C.c_size_t,
                                                 C.c_char_p, C.c_uint]
@@ -485,13 +490,13 @@ class Codec:
         return int(lib().qhuff_enc_str_size(self._ctx, s, len(s)))
 
     def huff_decode(self, src, dst_len=None, state=None, final=1):
-        """qhuff_huff_decode (lsqpack_huff_decode's arguments on this
+        """qhuff_huff_decode_ex (lsqpack_huff_decode's arguments on this
         context) -> (status, dst bytes [:n_dst], n_src)."""
         if dst_len is None:
             dst_len = len(src) * 8 // 5 + 1
         s = C.create_string_buffer(bytes(src), len(src) + 1)
         d = C.create_string_buffer(max(dst_len, 1))
         st = state if state is not None else DecodeState(0, 0, 0)
-        rv = lib().qhuff_huff_decode(self._ctx, s, len(src), d, dst_len,
-                                     C.byref(st), final)
+        rv = lib().qhuff_huff_decode_ex(self._ctx, s, len(src), d, dst_len,
+                                        C.byref(st), final)
         return rv.status, d.raw[:rv.n_dst], rv.n_src

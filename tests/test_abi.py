@@ -2,6 +2,7 @@
 loads, exports every entry point include/qhuff.h declares, and its host-only
 helpers behave.  No kernel is launched here (no GPU in the build container)."""
 import ctypes as C
+import os
 import re
 import subprocess
 
@@ -9,6 +10,7 @@ import numpy as np
 import pytest
 
 import _paths  # noqa: F401
+from _paths import ROOT
 import qhuff
 
 
@@ -42,7 +44,7 @@ def test_library_has_gfx950_code_object():
 def test_header_is_plain_c():
     """The boundary headers must compile as C99 with no HIP/torch types."""
     src = "".join('#include "%s"\n' % h for h in qhuff.HEADERS) + \
-        "int main(void){return QHUFF_ABI_VERSION != 1;}\n"
+        "int main(void){return QHUFF_ABI_VERSION != 2;}\n"
     r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-x", "c",
                         "-fsyntax-only", "-"], input=src, text=True,
                        capture_output=True)
@@ -108,3 +110,15 @@ def test_shard_cuts_balance():
     assert cuts[0] == 0 and cuts[-1] == 3 and np.all(np.diff(cuts.astype(int)) >= 0)
     cuts = qhuff.shard_cuts(np.array([0], dtype=np.uint32), 4)
     assert list(cuts) == [0, 0, 0, 0, 0]
+
+
+def test_abi_version_matches_header():
+    """the loaded library reports the header's QHUFF_ABI_VERSION (no device
+    needed); ABI 2 keeps version 1's 5-argument qhuff_huff_decode beside
+    qhuff_huff_decode_ex"""
+    assert qhuff.lib().qhuff_abi_version() == 2
+    src = open(os.path.join(ROOT, "include", "qhuff.h")).read()
+    assert "#define QHUFF_ABI_VERSION 2" in src
+    assert "qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, " \
+           "int src_len,\n                  unsigned char *dst, int dst_len);" \
+        in src

@@ -104,3 +104,47 @@ def test_one_context_two_streams(batch):
         assert np.array_equal(eo[:int(eoo[-1])].cpu().numpy(), h)
     assert c.device_error() == 0
     c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [100_000, 150_000])
+def test_two_contexts_concurrent_small(n):
+    """Batches of at most one tile per wave (the single-ticket prologue,
+    ADVICE r02): two contexts on two streams, several rounds back to back.
+    Each wave claims its second ticket itself, so whichever workgroups are
+    resident can fill a gap in any ticket group: no spin-limit error."""
+    import torch
+    import qhuff
+    data, off = qhuff.synth_batch(n, seed=n)
+    h, ho = O.encode_batch(data, off, 0)
+    c1, c2 = qhuff.Codec(0), qhuff.Codec(0)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    d = _dev(data, torch)
+    o = _dev(off.view(np.int32), torch)
+    hd = _dev(h, torch)
+    hod = _dev(ho.view(np.int32), torch)
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(6):
+        for c, s in ((c1, s1), (c2, s2)):
+            eo = torch.empty(qhuff.encode_bound(len(data), n, 0),
+                             dtype=torch.uint8, device="cuda")
+            eoo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+            do = torch.empty(qhuff.decode_bound(len(h), n), dtype=torch.uint8,
+                             device="cuda")
+            doo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+            st = torch.empty(n, dtype=torch.uint8, device="cuda")
+            c.encode_into(d, o, n, 0, eo, eoo, s)
+            c.decode_into(hd, hod, n, do, doo, st, s)
+            outs.append((eo, eoo, do, doo, st))
+    torch.cuda.synchronize()
+    assert c1.device_error() == 0 and c2.device_error() == 0
+    for eo, eoo, do, doo, st in outs:
+        eoo = eoo.cpu().numpy().view(np.uint32)
+        assert np.array_equal(eoo, ho)
+        assert np.array_equal(eo[:int(eoo[-1])].cpu().numpy(), h)
+        assert np.array_equal(doo.cpu().numpy().view(np.uint32), off)
+        assert not st.cpu().numpy().any()
+        assert np.array_equal(do[:len(data)].cpu().numpy(), data)
+    c1.close()
+    c2.close()

@@ -313,6 +313,17 @@ def test_host_path_and_mirrors(codec):
     st, out, _ = codec.huff_decode(bytes.fromhex("f1e3c2f51531a245cf64df"),
                                    dst_len=4)
     assert st == 2
+    # ABI 1's 5-argument qhuff_huff_decode: a complete string, same results
+    import ctypes as C
+    import qhuff
+    L = qhuff.lib()
+    for src, dl in ((bytes.fromhex("f1e3c2f51531a245cf64df"), 64),
+                    (b"\xff", 64),
+                    (bytes.fromhex("f1e3c2f51531a245cf64df"), 4)):
+        d = C.create_string_buffer(dl)
+        rv = L.qhuff_huff_decode(codec._ctx, src, len(src), d, dl)
+        st, out, n_src = codec.huff_decode(src, dst_len=dl)
+        assert (rv.status, d.raw[:rv.n_dst], rv.n_src) == (st, out, n_src)
 
 
 def test_host_path_pipelined_chunks(codec):
