@@ -30,10 +30,12 @@ struct qhuff_memo
     struct table et;
     uint8_t *e_str, *e_huf;
     uint32_t *e_str_off, *e_huf_off;
-    /* decoder: decoded strings and status per literal */
+    /* decoder: the Huffman payloads (copied, to check they did not change:
+     * a receive buffer reused at the same address must not hit), decoded
+     * strings and status per literal */
     struct table dt;
-    uint8_t *d_out, *d_st;
-    uint32_t *d_off;
+    uint8_t *d_src, *d_out, *d_st;
+    uint32_t *d_src_off, *d_off;
 };
 
 static __thread struct qhuff_memo *t_memo;
@@ -109,12 +111,14 @@ enc_clear(struct qhuff_memo *m)
 static void
 dec_clear(struct qhuff_memo *m)
 {
+    free(m->d_src);
+    free(m->d_src_off);
     free(m->d_out);
     free(m->d_st);
     free(m->d_off);
     free(m->dt.s);
-    m->d_out = m->d_st = NULL;
-    m->d_off = NULL;
+    m->d_src = m->d_out = m->d_st = NULL;
+    m->d_src_off = m->d_off = NULL;
     m->dt.s = NULL;
 }
 
@@ -178,10 +182,18 @@ qhuff_memo_decode(struct qhuff_memo *m, const unsigned char *buf,
 {
     dec_clear(m);
     const uint64_t ob = qhuff_literals_bound(lits, n);
+    uint64_t sb = 0;
+    for (unsigned i = 0; i < n; ++i)
+        sb += lits[i].huffman ? lits[i].len : 0;
+    if (sb >= 0xffffffffull)
+        return QHUFF_ERANGE;
+    m->d_src = malloc(sb ? sb : 1);
+    m->d_src_off = malloc((n + 1) * sizeof *m->d_src_off);
     m->d_out = malloc(ob ? ob : 1);
     m->d_st = malloc(n ? n : 1);
     m->d_off = malloc((n + 1) * sizeof *m->d_off);
-    if (!m->d_out || !m->d_st || !m->d_off || table_init(&m->dt, n))
+    if (!m->d_src || !m->d_src_off || !m->d_out || !m->d_st || !m->d_off
+            || table_init(&m->dt, n))
     {
         dec_clear(m);
         return QHUFF_ENOMEM;
@@ -193,9 +205,18 @@ qhuff_memo_decode(struct qhuff_memo *m, const unsigned char *buf,
         dec_clear(m);
         return rc;
     }
+    uint32_t o = 0;
     for (unsigned i = 0; i < n; ++i)
+    {
+        m->d_src_off[i] = o;
         if (lits[i].huffman)        /* the reference decodes only these */
+        {
+            memcpy(m->d_src + o, buf + lits[i].pos, lits[i].len);
+            o += lits[i].len;
             table_put(&m->dt, buf + lits[i].pos, lits[i].len, i);
+        }
+    }
+    m->d_src_off[n] = o;
     return QHUFF_OK;
 }
 
@@ -260,8 +281,9 @@ lsqpack_qhuff_dec_lookup(const unsigned char *src, int src_len,
     if (!m || src_len < 0 || dst_len < 0)
         return 0;
     const struct slot *s = table_get(&m->dt, src, (unsigned) src_len);
-    if (!s || m->d_st[s->idx] != QHUFF_DEC_OK)
-        return 0;
+    if (!s || m->d_st[s->idx] != QHUFF_DEC_OK
+            || memcmp(m->d_src + m->d_src_off[s->idx], src, (size_t) src_len))
+        return 0;                   /* not memoised, or the bytes changed */
     const uint32_t n = m->d_off[s->idx + 1] - m->d_off[s->idx];
     /* With room to spare the reference returns OK whichever of its decoders
      * runs (neither can reach its dst_ended condition); at n >= dst_len its

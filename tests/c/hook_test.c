@@ -258,6 +258,24 @@ run_dec(struct qhuff_memo *m, const char *path)
                   "huff_decode", i, (unsigned) dl);
         }
     }
+    /* a receive buffer reused at the same address: once the
+     * bytes under a memoised payload change, the lookup must miss */
+    for (uint32_t i = 0; i < n; ++i)
+        if (lits[i].huffman && lits[i].len)
+        {
+            unsigned char *p = buf + lits[i].pos;
+            const int sl = (int) lits[i].len;
+            const unsigned char keep = p[0];
+            struct qhuff_decode_retval rv;
+            const int before = lsqpack_qhuff_dec_lookup(p, sl, got, sizeof got,
+                                                        &rv);
+            p[0] ^= 0x5a;
+            check(!lsqpack_qhuff_dec_lookup(p, sl, got, sizeof got, &rv),
+                  "stale payload hit", i, 0);
+            p[0] = keep;
+            check(lsqpack_qhuff_dec_lookup(p, sl, got, sizeof got, &rv)
+                  == before, "restored payload", i, 0);
+        }
     printf("dec %s: literals %u (huffman %u)\n", path, n, n_huff);
     free(lits);
     free(buf);
