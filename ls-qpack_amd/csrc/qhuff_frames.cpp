@@ -13,8 +13,7 @@
 // pinned batch and decoded by the GPU kernel in a single launch.  Dynamic
 // table references, blocked streams and the decoder's state machine stay
 // with the reference: the scan resolves no index and allocates nothing.
-#include <hip/hip_runtime.h>
-
+// Plain C++ (no HIP): tests/c/ also builds it with ASan/UBSan on the CPU.
 #include <stdint.h>
 #include <string.h>
 

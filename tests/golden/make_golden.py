@@ -16,6 +16,9 @@ Sources (all under /root/reference):
   lsqpack.c                  static_table[] (QPACK static table, data)
   fuzz/input/256.100.1/*     interop-encode output, -t 256 -s 100 -a 1
   test/qifs/*.qif            QIF corpora the streams above were encoded from
+  fuzz/decode/{a,b,c,d}/*    AFL seed corpora of the decoder (preambles and
+                             test cases, copied as data/fuzz/*; names and
+                             harness in fuzz_decode.json)
 
 Output: kat_*.json (hex strings + source file:line), and copies of the data
 files under tests/golden/data/.  A SHA-256 manifest is written to
@@ -309,8 +312,52 @@ def main():
             shutil.copyfile(os.path.join(d, fn), os.path.join(data, fn))
             copied.append(os.path.join("data", fn))
 
+    # AFL seed corpora of the decoder (fuzz/decode/{a,b,c,d}): each dir's
+    # preamble (if any) and test cases, renamed to safe names; the manifest
+    # keeps the original names and the harness each dir is run with
+    # (fuzz/decode/*/README, setup.sh; bin/fuzz-decode.c:152-202 framing)
+    harness = {
+        "a": {"program": "fuzz-decode", "table_size": 256, "risked": 100},
+        "b": {"program": "fuzz-decode", "table_size": 4096, "risked": 100},
+        "c": {"program": "interop-decode", "table_size": 256, "risked": 100},
+        "d": {"program": "fuzz-decode", "table_size": 256, "risked": 100},
+    }
+    fz = {"source": "fuzz/decode/*", "framing":
+          "records of u64 BE stream id, u32 BE size, payload (stream 0 = "
+          "encoder stream); fuzz-decode: preamble strict, all records, then "
+          "the test case's FIRST record with its size clamped to the file "
+          "(bin/fuzz-decode.c:152-202, 331-332); interop-decode: every "
+          "record of the test case", "dirs": {}}
+    for sub in sorted(harness):
+        d = os.path.join(REF, "fuzz/decode", sub)
+        dst = os.path.join(data, "fuzz", sub)
+        os.makedirs(dst, exist_ok=True)
+        ent = dict(harness[sub], preamble=None, cases=[])
+        if os.path.exists(os.path.join(d, "preamble")):
+            shutil.copyfile(os.path.join(d, "preamble"),
+                            os.path.join(dst, "preamble"))
+            ent["preamble"] = "data/fuzz/%s/preamble" % sub
+            copied.append(os.path.join("data", "fuzz", sub, "preamble"))
+        tc = os.path.join(d, "test-cases")
+        for k, fn in enumerate(sorted(os.listdir(tc))):
+            safe = "case%02d" % k
+            shutil.copyfile(os.path.join(tc, fn), os.path.join(dst, safe))
+            ent["cases"].append({"file": "data/fuzz/%s/%s" % (sub, safe),
+                                 "original": "fuzz/decode/%s/test-cases/%s"
+                                             % (sub, fn)})
+            copied.append(os.path.join("data", "fuzz", sub, safe))
+        fz["dirs"][sub] = ent
+    out["fuzz_decode.json"] = fz
+    with open(os.path.join(HERE, "fuzz_decode.json"), "w") as fp:
+        json.dump(fz, fp, indent=1, sort_keys=True)
+        fp.write("\n")
+
+    # fixtures written by the other generator (make_xxh32_golden.py) keep
+    # their manifest lines
+    others = [fn for fn in ("xxh32.json",)
+              if os.path.exists(os.path.join(HERE, fn))]
     man = []
-    for fn in sorted(list(out) + copied):
+    for fn in sorted(list(out) + copied + others):
         h = hashlib.sha256(open(os.path.join(HERE, fn), "rb").read()).hexdigest()
         man.append("%s  %s" % (h, fn))
     with open(os.path.join(HERE, "MANIFEST.sha256"), "w") as fp:

@@ -39,7 +39,9 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        L = C.CDLL(build())
+        # QHUFF_ORACLE_LIB: another build of the same oracle (the
+        # sanitizer run, tests/test_sanitize.py)
+        L = C.CDLL(os.environ.get("QHUFF_ORACLE_LIB") or build())
         u8p = C.POINTER(C.c_uint8)
         L.oq_enc_str_size.restype = C.c_uint
         L.oq_enc_str_size.argtypes = [C.c_char_p, C.c_uint]

@@ -168,3 +168,148 @@ def qif_header_lists(text):
     if cur:
         lists.append(cur)
     return lists
+
+
+# ---- strict restatement of the reference's framing rules (for the scanner
+# tests on adversarial input: the reference's AFL seed corpora) -------------
+
+class ProtoError(Exception):
+    """lsqpack_dec_int / _int24 return -2 (lsqpack.c:2423, 2435, 2459)."""
+
+
+MASK64 = (1 << 64) - 1
+
+
+def dec_int(buf, pos, prefix_bits):
+    """lsqpack_dec_int (lsqpack.c:2372-2436) on a complete buffer -> (value,
+    pos); Truncated (-1) when the buffer ends inside the integer (within one
+    call fewer than LSQPACK_UINT64_ENC_SZ = 11 bytes are read before that
+    can happen, 2413-2420), ProtoError (-2) when the value needs more than
+    64 bits (2426-2435)."""
+    if pos >= len(buf):
+        raise Truncated()
+    pmax = (1 << prefix_bits) - 1
+    val = buf[pos] & pmax
+    pos += 1
+    if val < pmax:
+        return val, pos
+    M = 0
+    while True:
+        if pos >= len(buf):
+            raise Truncated()
+        B = buf[pos]
+        pos += 1
+        val = (val + ((B & 0x7F) << M)) & MASK64
+        M += 7
+        if not (B & 0x80 and M < 64):
+            break
+    if M <= 63 or (M == 70 and buf[pos - 1] <= 1 and val >> 63):
+        return val, pos
+    raise ProtoError()
+
+
+def dec_int24(buf, pos, prefix_bits):
+    """lsqpack_dec_int24 (lsqpack.c:2443-2460): values >= 2^24 fail (-2)."""
+    v, pos = dec_int(buf, pos, prefix_bits)
+    if v >= 1 << 24:
+        raise ProtoError()
+    return v, pos
+
+
+def _lit(buf, pos, prefix_bits, kind, instr):
+    if pos >= len(buf):
+        raise Truncated()
+    h = (buf[pos] >> prefix_bits) & 1
+    n, p = dec_int24(buf, pos, prefix_bits)
+    if p + n > len(buf):
+        raise Truncated()
+    return (p, n, h, prefix_bits, p - pos, kind, instr), p + n
+
+
+LIT_NAME, LIT_VALUE = 1, 2
+
+
+def ref_scan_field_section(buf):
+    """Literal spans of one field section under the reference's integer rules
+    (RFC 9204 4.5; parse_header_prefix / parse_header_data, lsqpack.c:
+    3955-4046, 3567-3915) -> ("ok" | "trunc" | "proto", [(pos, len, huffman,
+    prefix_bits, hdr_len, kind, instr)])."""
+    lits = []
+    try:
+        _, pos = dec_int(buf, 0, 8)            # Required Insert Count
+        _, pos = dec_int(buf, pos, 7)          # S + Delta Base
+        while pos < len(buf):
+            b, at = buf[pos], pos
+            if b & 0x80:                       # indexed field line
+                _, pos = dec_int24(buf, pos, 6)
+            elif b & 0x40:                     # literal with name reference
+                _, pos = dec_int24(buf, pos, 4)
+                lit, pos = _lit(buf, pos, 7, LIT_VALUE, at)
+                lits.append(lit)
+            elif b & 0x20:                     # literal with literal name
+                n, pos = _lit(buf, pos, 3, LIT_NAME, at)
+                v, pos = _lit(buf, pos, 7, LIT_VALUE, at)
+                lits += [n, v]
+            elif b & 0x10:                     # indexed post-base
+                _, pos = dec_int24(buf, pos, 4)
+            else:                              # post-base name reference
+                _, pos = dec_int24(buf, pos, 3)
+                lit, pos = _lit(buf, pos, 7, LIT_VALUE, at)
+                lits.append(lit)
+    except Truncated:
+        return "trunc", []
+    except ProtoError:
+        return "proto", []
+    return "ok", lits
+
+
+def ref_scan_encoder_stream(buf):
+    """Literal spans of the complete encoder-stream instructions in buf
+    (RFC 9204 4.3; lsqpack_dec_enc_in, lsqpack.c:4574-4960: name index and
+    lengths by dec_int24, capacity by dec_int, duplicate by dec_int24) ->
+    ("ok" | "proto", [spans], consumed); a partial last instruction is left
+    unconsumed (the reference resumes there)."""
+    lits, pos = [], 0
+    while pos < len(buf):
+        b, at, q = buf[pos], pos, pos
+        got = []
+        try:
+            if b & 0x80:                       # insert with name reference
+                _, q = dec_int24(buf, q, 6)
+                lit, q = _lit(buf, q, 7, LIT_VALUE, at)
+                got.append(lit)
+            elif b & 0x40:                     # insert with literal name
+                n, q = _lit(buf, q, 5, LIT_NAME, at)
+                v, q = _lit(buf, q, 7, LIT_VALUE, at)
+                got += [n, v]
+            elif b & 0x20:                     # set dynamic table capacity
+                _, q = dec_int(buf, q, 5)
+            else:                              # duplicate
+                _, q = dec_int24(buf, q, 5)
+        except Truncated:
+            break
+        except ProtoError:
+            return "proto", [], 0
+        lits += got
+        pos = q
+    return "ok", lits, pos
+
+
+def fuzz_records(data, strict=True, single=False):
+    """Records as bin/fuzz-decode.c:152-202 reads them: u64 BE stream id, u32
+    BE size, payload, while more than 12 bytes remain; a size past the end
+    is clamped (non-strict) or ends the walk (strict: the reference aborts);
+    single: the first record only."""
+    out, pos = [], 0
+    while pos + 12 < len(data):
+        sid, size = struct.unpack(">QI", data[pos:pos + 12])
+        pos += 12
+        if size > len(data) - pos:
+            if strict:
+                raise ValueError("truncated preamble at %d" % pos)
+            size = len(data) - pos
+        out.append((sid, bytes(data[pos:pos + size])))
+        pos += size
+        if single:
+            break
+    return out
