@@ -9,130 +9,55 @@
 //      (lsqpack.c:5362-5426, 3482-3497)
 //
 // One string per lane, one 64-string tile per wave (qhuff_device.h).  The
-// tile's input is staged in the wave's LDS region as big-endian dwords;
-// each lane keeps a 64-bit bit buffer in registers, refilled from the stage
-// one aligned dword at a time (the refill read is independent of the table
-// lookup, so one LDS round trip sits on the per-step dependency chain).  A
-// step looks the top 13 bits up in a window table (up to two symbols of
-// <= 13 bits); codes of 14..30 bits take a canonical length search behind a
-// wave-uniform branch.  While >= 32 real bits remain the step needs no
-// padding or tail logic; the last < 32 bits run a careful epilogue that
-// pads with ones (as huff_decode_fast pads its last window,
-// lsqpack.c:5364-5365) and applies the D3 rule.
+// tile's Huffman input is staged in the wave's LDS region as big-endian
+// dwords.  Each lane holds its bit stream as two dwords A:B and a bit
+// position (decode_string_lds): a step looks the next 13 bits up in a window
+// table (up to two symbols of <= 13 bits), writes the entry's two symbol
+// bytes to the string's arena slot and advances by the bits consumed.
+// Codes of 14..30 bits stall their lane and are decoded together outside the
+// step loop by a canonical length search.  Main steps run while the lane has
+// >= 13 real bits; the last < 13 bits (at most two symbols) take a padded
+// one-lookup epilogue that applies the D3 tail rule (fewer than 8 padding
+// bits, all ones).
 //
-// Output bytes land in a byte-granular per-string arena slot.  After the
-// wave scan of the sizes they are compacted into the (now dead) input stage
-// and copied out with 16-byte stores once the look-back has resolved the
-// tile's output base.
+// After the wave scan of the output sizes the arena slots are compacted
+// into the (now dead) input stage and copied out with 16-byte stores once
+// the look-back has resolved the tile's output base.
 #include "qhuff_pipeline.h"
 
 #ifndef QH_DEPTH
 #define QH_DEPTH 3
 #endif
-#ifndef QH_BORROW
-#define QH_BORROW 1
-#endif
 // bytes past the last slot's bound (the two-byte emitter writes one past
-// its end): 16 keeps a wave's region at 8,128 B, so 16 waves + the tables fit
-// the 160 KiB of LDS
+// its end)
 #ifndef QH_ARENA_SLACK
 #define QH_ARENA_SLACK 16
-#endif
-#ifndef QH_ADDR
-#define QH_ADDR 1
-#endif
-#ifndef QH_NXCOND
-#define QH_NXCOND 0
-#endif
-// two main-loop steps per trip, one refill read per trip, dword emitter
-// (decode_string_lds).  Parity-green on MI355X but slower: codec 12.5k vs
-// 10.6k cycles per tile, dec 74.3 vs 68.3 us (profiles/r02_j) -- halving the
-// codec's LDS operations did not pay for ~35 % more VALU per step, so the
-// loop is not bound by LDS throughput.  Off.
-#ifndef QH_PAIR
-#define QH_PAIR 0
-#endif
-#ifndef QH_TAIL1
-#define QH_TAIL1 1
-#endif
-#ifndef QH_COMPACT8
-#define QH_COMPACT8 1
-#endif
-#ifndef QH_COMPACT64
-#define QH_COMPACT64 0
-#endif
-// long codes stall their lane and are decoded outside the step loop (no
-// long-code branch in the step)
-#ifndef QH_STALL
-#define QH_STALL 1
-#endif
-#if QH_STALL && !QH_ADDR
-#error "QH_STALL needs QH_ADDR"
-#endif
-#if QH_PAIR && !QH_ADDR
-#error "QH_PAIR needs QH_ADDR"
-#endif
-#ifndef QH_EMITCOND
-#define QH_EMITCOND 0
 #endif
 
 namespace qhuff {
 
-// QH_NSBYTE: the LDS copy of the window table drops the entries' 32 - c
-// field ([31:26], masked off in the prologue), so the symbol count is the
-// whole top byte and the arena pointer advances by one SDWA add (byte 3 of
-// the entry as the operand) instead of a bfe + add.  The hold entry is then
-// 0 (c = 0, ns = 0): only the STALL loop may use it (it never tests a held
-// lane's entry for a long code).
-#ifndef QH_NSBYTE
-#define QH_NSBYTE 0
-#endif
-#if QH_NSBYTE && (!QH_STALL || QH_DUAL || QH_PAIR)
-#error "QH_NSBYTE needs the QH_STALL loop (not QH_DUAL / QH_PAIR)"
-#endif
 
 // window entry fields (qhuff_tables.h)
 __device__ __forceinline__ uint32_t ent_c(uint32_t e) { return (e >> 8) & 15; }
 __device__ __forceinline__ uint32_t ent_l0(uint32_t e) { return (e >> 12) & 15; }
-__device__ __forceinline__ uint32_t ent_ns(uint32_t e)
-{
-    return QH_NSBYTE ? e >> 24 : (e >> 24) & 3;
-}
+__device__ __forceinline__ uint32_t ent_ns(uint32_t e) { return (e >> 24) & 3; }
 __device__ __forceinline__ uint32_t ent_sym1(uint32_t e) { return (e >> 16) & 0xff; }
 
 // staged input bytes (the output stage, the dead input stage, always has the
-// chunk registers' 3,072).  2,816 lets 16 waves (4 per SIMD, <= 128 VGPRs)
-// fit the LDS -- measured slower than 12 waves (dec 88 vs 86 us: the codec
-// is issue-bound and the look-backs wait longer), so the default is the
-// full 3,072 at 12 waves.
-// QH_DUAL: 128-string tiles, two strings per lane (2l and 2l + 1) decoded
-// as two interleaved chains, 6 chunks (6,144 B) of stage per wave, run at 8
-// waves per workgroup (the Makefile's dual build).
-#ifndef QH_DUAL
-#define QH_DUAL 0
-#endif
-#if QH_DUAL && QH_PAIR
-#error "QH_DUAL and QH_PAIR are exclusive"
-#endif
-constexpr bool kDual = QH_DUAL;
-constexpr int kDecNch = kDual ? 6 : kChunks;            // chunks per lane
-constexpr uint32_t kDecTS = kDual ? 2 * kWT : kWT;      // strings per tile
+// chunk registers' 3,072); a smaller cap lets more waves fit the LDS (16
+// waves at 2,816 B were slower: dec 88 vs 86 us, round 1)
+constexpr int kDecNch = kChunks;                        // chunks per lane
+constexpr uint32_t kDecTS = kWT;                        // strings per tile
 constexpr int kDecStageCap = 64 * kDecNch * 16;
 #ifndef QH_DEC_IN_CAP
-#define QH_DEC_IN_CAP (QH_DUAL ? 5632 : 3072)
+#define QH_DEC_IN_CAP 3072
 #endif
 constexpr int kDecInCap = QH_DEC_IN_CAP;
 static_assert(kDecInCap % 16 == 0 && kDecInCap <= kDecStageCap, "input cap");
 // byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
 // most 8/5 of its input, plus one byte written past the end by the
 // two-byte emitter
-#if QH_PAIR
-// dword slot of string i: i + floor(2 * (rs_i - A) / 5) -- its output is at
-// most floor(8 len / 5) bytes, ceil(that / 4) <= floor(2 len / 5) + 1 dwords
-constexpr int kArenaBytes = 4 * (kWT + 2 * kDecInCap / 5 + 2);
-#else
 constexpr int kArenaBytes = 2 * kDecTS + 8 * kDecInCap / 5 + QH_ARENA_SLACK;
-#endif
 
 struct DecWave                       // one wave's private LDS region
 {
@@ -142,7 +67,7 @@ struct DecWave                       // one wave's private LDS region
 
 // hold entry, one past the window table: c = 0, ns = 0, not a long code
 constexpr uint32_t kHoldIdx = kWinSize;
-constexpr uint32_t kHoldEntry = QH_NSBYTE ? 0u : 1u << 26;
+constexpr uint32_t kHoldEntry = 1u << 26;
 
 struct DecSmem
 {
@@ -216,11 +141,6 @@ main_step(bool act, uint32_t d, uint32_t &hi, uint32_t &lo, uint32_t &bits,
 {
     uint32_t e = s_win[hi >> (32 - kWinBits)];
     bool ok = true;
-#if QH_NSBYTE
-    // (the LDS entries carry no 32 - c field: bits consumed kept apart;
-    // cc = 32 for an empty step, as the field's 0 gave)
-    uint32_t cb = ent_c(e);
-#endif
     if (__builtin_amdgcn_ballot_w64((GATED ? act : true) & (e < (1u << 24))))
     {
         // a code of 13..30 bits: synthesize the entry of a one-symbol step
@@ -231,20 +151,11 @@ main_step(bool act, uint32_t d, uint32_t &hi, uint32_t &lo, uint32_t &bits,
         const uint32_t el = (sym & 0xff) | (L << 8) | (L << 12) | (1u << 24)
                           | ((32u - L) << 26);
         e = lng ? (ok ? el : 0u) : e;
-#if QH_NSBYTE
-        cb = lng ? (ok ? L : 0u) : cb;
-#endif
     }
     if (GATED)
         e = act ? e : 0u;
     const uint32_t nb = (e >> 24) & 3;       // 0 for a held lane
-#if QH_NSBYTE
-    if (GATED)
-        cb = act ? cb : 0u;
-    const uint32_t k = (32u - cb) & 31;      // 32 - bits consumed (0: none)
-#else
     const uint32_t k = e >> 26;              // 32 - bits consumed
-#endif
     const uint32_t cc = 32u - k;
     emit(e, nb);
     const uint32_t sh = __builtin_amdgcn_alignbit(hi, lo, k);
@@ -382,97 +293,22 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         nx = src[p];
     }
     uint32_t bad = 0;                        // (a u32: no lane-mask phis)
-    // One loop, no lane branches: a lane with < kWinBits real bits left
+    // No lane branches in the step: a lane with < kWinBits real bits left
     // looks up the hold entry (c = ns = 0, never a long code); its two arena
     // byte writes land at its current end and are overwritten by the
-    // epilogue.  The long-code fix is computed for the whole wave with
-    // selects, behind a wave-uniform branch.
+    // epilogue.
     constexpr uint32_t kMain = kWinBits;
     uint32_t W = __builtin_amdgcn_alignbit(A, B, t);
-#if QH_ADDR
     // idx is the entry's byte offset: (W >> 17) & 0x7ffc for a live lane,
     // the hold entry's for a held one -- one v_and_or on the step's chain
-    // (the two masks come off the rem compare, beside it)
+    // (the two masks come off the rem compare, beside it).  (One select
+    // after the masked shift, a VALU fewer but one longer on the chain, was
+    // neutral: dec 66.16 vs 66.21 us, profiles/r02_r/ab_addr2.txt.)
     auto win_addr = [](uint32_t w, bool live) -> uint32_t {
-#if QH_ADDR == 2
-        // one select after the masked shift: 3 VALU (lshr, and, cndmask)
-        // instead of 4 (two mask selects, lshr, and_or) -- the step is close
-        // to VALU-issue-bound, its dependency chain is one op longer
-        return live ? (w >> (32 - kWinBits - 2)) & (4u * (kWinSize - 1))
-                    : 4u * kHoldIdx;
-#else
         return ((w >> (32 - kWinBits - 2)) & (live ? 4u * (kWinSize - 1) : 0u))
              | (live ? 0u : 4u * kHoldIdx);
-#endif
     };
     uint32_t idx = win_addr(W, rem >= kMain);
-#else
-    uint32_t idx = rem >= kMain ? W >> (32 - kWinBits) : kHoldIdx;
-#endif
-#if QH_PAIR
-    // Two steps per trip.  The refill read is issued once per trip: after a
-    // step of <= 13 bits that moved the window on a dword (t went from t0 to
-    // t0 - c + 32 >= 19), the next such step cannot move it again, so one
-    // prefetched dword serves both; a long code (<= 30 bits) re-reads it in
-    // its (wave-uniform) branch.  The symbol bytes of both steps are appended
-    // to the lane's dword accumulator together (Emit::put2): an aligned
-    // ds_write_b32 per four output bytes instead of two byte writes per step
-    // -- the codec's LDS cycles, not its VALU, bound it at 12 waves/CU.
-    auto lds_at = [&](uint32_t a) -> uint32_t {
-        return *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + a);
-    };
-    auto advance = [&](uint32_t c) {
-        uint32_t tn;
-        const bool cross = __builtin_sub_overflow(t, c, &tn);
-        A = cross ? B : A;
-        B = cross ? nx : B;
-        t = tn & 31;
-        p += cross ? 1u : 0u;
-    };
-    // long-code fix of a step whose entry e is a long-code marker (lanes
-    // with e >= 2^24 keep e, c, s)
-    auto long_fix = [&](uint32_t &e, uint32_t &c, uint32_t &sb) {
-        const bool lng = e < (1u << 24);
-        uint32_t L;
-        const uint32_t sym = long_code(W, s_sorted, &L);
-        const bool rej = lng & ((sym == 256) | (L > rem));
-        e = lng ? (rej ? 0u : sym) : e;
-        c = lng ? (rej ? 0u : L) : c;
-        sb = lng ? (rej ? 0u : 8u) : sb;
-        bad |= rej ? 1u : 0u;
-        rem = rej ? 0u : rem;
-    };
-    if (__builtin_amdgcn_ballot_w64(rem >= kMain))
-    do
-    {
-        uint32_t e1 = lds_at(idx);
-        uint32_t c1 = ent_c(e1);
-        uint32_t s1 = (e1 >> 21) & 0x18u;    // 8 * symbols
-        const bool lg1 = __builtin_amdgcn_ballot_w64(e1 < (1u << 24)) != 0;
-        if (__builtin_expect(lg1, 0))
-            long_fix(e1, c1, s1);
-        rem -= c1;
-        advance(c1);
-        W = __builtin_amdgcn_alignbit(A, B, t);
-        idx = win_addr(W, rem >= kMain);
-        if (__builtin_expect(lg1, 0))
-            nx = src[p];                     // a long step may have crossed
-        uint32_t e2 = lds_at(idx);
-        uint32_t c2 = ent_c(e2);
-        uint32_t s2 = (e2 >> 21) & 0x18u;
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(e2 < (1u << 24)) != 0, 0))
-        {
-            nx = src[p];                     // step 1 may have crossed
-            long_fix(e2, c2, s2);
-        }
-        rem -= c2;
-        advance(c2);
-        nx = src[p];
-        W = __builtin_amdgcn_alignbit(A, B, t);
-        idx = win_addr(W, rem >= kMain);
-        emit.put2(e1, s1, e2, s2);
-    } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
-#elif QH_STALL
     // A long-code marker entry (e < 2^24: c = ns = 0) stalls its lane where
     // it is, like the hold entry.  The step loop runs while some lane with
     // >= kMain bits left is not stalled -- so the step carries no long-code
@@ -519,67 +355,7 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         W = __builtin_amdgcn_alignbit(A, B, t);
         idx = win_addr(W, rem >= kMain);
     }
-#else
-    if (__builtin_amdgcn_ballot_w64(rem >= kMain))
-    do
-    {
-#if QH_ADDR
-        uint32_t e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
-#else
-        uint32_t e = s_win[idx];
-#endif
-        uint32_t c = ent_c(e);                // bits of the entry's symbols
-        uint32_t ns = ent_ns(e);              // symbols (0: longer code)
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(e < (1u << 24)) != 0, 0))
-        {
-            // a code of 14..30 bits; EOS, or a code running past the end,
-            // rejects the string (D3)
-            const bool lng = e < (1u << 24);
-            uint32_t L;
-            const uint32_t sym = long_code(W, s_sorted, &L);
-            const bool rej = lng & ((sym == 256) | (L > rem));
-            e = lng ? sym : e;
-            c = lng ? (rej ? 0u : L) : c;
-            ns = lng ? (rej ? 0u : 1u) : ns;
-            bad |= rej ? 1u : 0u;
-            rem = rej ? 0u : rem;
-        }
-        emit(e, ns);
-        rem -= c;
-#if QH_BORROW
-        // t - c borrows exactly when the window moves on a dword: one
-        // v_sub_co for both, the borrow (vcc) feeding the selects and p
-        uint32_t tn;
-        const bool cross = __builtin_sub_overflow(t, c, &tn);
-        A = cross ? B : A;
-        B = cross ? nx : B;
-        t = tn & 31;
-        p += cross ? 1u : 0u;
-#else
-        const int32_t tn = (int32_t) t - (int32_t) c;
-        const bool cross = tn < 0;
-        A = cross ? B : A;
-        B = cross ? nx : B;
-        t = (uint32_t) tn & 31;
-        p += cross ? 1u : 0u;
-#endif
-#if QH_NXCOND
-        if (cross)                           // exec-masked: crossing lanes only
-            nx = src[p];
-#else
-        nx = src[p];
-#endif
-        W = __builtin_amdgcn_alignbit(A, B, t);
-#if QH_ADDR
-        idx = win_addr(W, rem >= kMain);
-#else
-        idx = rem >= kMain ? W >> (32 - kWinBits) : kHoldIdx;
-#endif
-    } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
 
-#endif
-
-#if QH_TAIL1
     // epilogue, one pass: the last < kWinBits (13) real bits hold at most
     // two symbols (codes are >= 5 bits), both inside the window padded with
     // ones, so one lookup decodes them; the bits after them cannot complete
@@ -600,183 +376,8 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         const bool pad_ok = r2 < 8 && (r2 == 0 || (inv >> ((32 - r2) & 31)) == 0);
         bad |= (live & !pad_ok) ? 1u : 0u;
     }
-#else
-    // epilogue: the last < kWinBits bits, padded with ones; D3 tail rule
-    bool fin = bad || rem == 0;
-    if (__builtin_amdgcn_ballot_w64(!fin))
-    do
-    {
-        const uint32_t w = W | (0xffffffffu >> (rem & 31));
-        const uint32_t e = s_win[w >> (32 - kWinBits)];
-        const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
-        const bool two = (ns == 2) & (ct <= rem);
-        uint32_t c = two ? ct : (ns ? l0 : 31u);
-        uint32_t val = e;
-        bool eos = false;
-        if (__builtin_amdgcn_ballot_w64(!fin & (ns == 0) & (rem > kWinBits)))
-        {
-            uint32_t L;
-            const uint32_t sym = long_code(w, s_sorted, &L);
-            const bool lng = (ns == 0) & (rem > kWinBits);
-            c = lng ? L : c;
-            val = lng ? sym : val;
-            eos = lng & (sym == 256);
-        }
-        // c > rem: what is left is padding -- at most 7 bits of EOS prefix
-        const bool over = c > rem;
-        const uint32_t ones = 0xffffffffu >> ((32 - rem) & 31);
-        const bool tail_bad = rem >= 8 || (w >> ((32 - rem) & 31)) != ones;
-        const bool live = !fin;
-        bad |= (live & ((over & tail_bad) | (!over & eos))) ? 1u : 0u;
-        const bool step = live & !over & !eos;
-        const uint32_t nb = step ? (two ? 2u : 1u) : 0u;
-        c = step ? c : 0;
-        emit(val, nb);
-        rem -= c;
-        const int32_t tn = (int32_t) t - (int32_t) c;
-        const bool cross = tn < 0;
-        A = cross ? B : A;
-        B = cross ? nx : B;
-        t = (uint32_t) tn & 31;
-        W = __builtin_amdgcn_alignbit(A, B, t);
-        fin = fin | over | eos | (rem == 0);
-    } while (__builtin_amdgcn_ballot_w64(!fin));
-#endif
     emit.finish();
     return bad ? -1 : (int) emit.n;
-}
-
-// ---- QH_DUAL: two strings per lane ----------------------------------------
-
-// Lane l of a 128-string tile holds the offsets of strings 2l and 2l + 1 and
-// the end of 2l + 1 (indices clamped to the tile's count: lanes past it hold
-// empty strings at the tile end).
-struct TileOffs2
-{
-    uint32_t o0, o1, o2;
-
-    __device__ __forceinline__ void load(const QH_GLB uint32_t *in_off,
-                                         uint64_t s0, uint32_t cnt)
-    {
-        const uint32_t i0 = 2 * lane_id();
-        o0 = in_off[s0 + (i0 < cnt ? i0 : cnt)];
-        o1 = in_off[s0 + (i0 + 1 < cnt ? i0 + 1 : cnt)];
-        o2 = in_off[s0 + (i0 + 2 < cnt ? i0 + 2 : cnt)];
-    }
-    __device__ __forceinline__ uint32_t first() const { return read_lane(o0, 0); }
-    __device__ __forceinline__ uint32_t last() const { return read_lane(o2, 63); }
-};
-
-// One decode chain of decode_pair_lds: the state of decode_string_lds (the
-// A:B window at position t, the prefetched next dword, the window address)
-// and the lane's arena pointer.
-struct LdsChain
-{
-    uint32_t rem, A, B, t, p, nx, W, idx, bad;
-    QH_LDS uint8_t *slot, *q;
-
-    __device__ __forceinline__ static uint32_t win_addr(uint32_t w, bool live)
-    {
-        return ((w >> (32 - kWinBits - 2)) & (live ? 4u * (kWinSize - 1) : 0u))
-             | (live ? 0u : 4u * kHoldIdx);
-    }
-    __device__ __forceinline__ void init(const QH_LDS uint32_t *src,
-                                         uint32_t bit0, uint32_t bitend,
-                                         QH_LDS uint8_t *s)
-    {
-        rem = bitend - bit0;
-        const uint32_t i0 = bit0 >> 5, sk = bit0 & 31;
-        A = src[i0];
-        const uint32_t a1 = src[i0 + 1];
-        B = sk ? a1 : A;
-        t = (32 - sk) & 31;
-        p = sk ? i0 + 2 : i0 + 1;
-        nx = src[p];
-        bad = 0;
-        slot = q = s;
-        W = __builtin_amdgcn_alignbit(A, B, t);
-        idx = win_addr(W, rem >= kWinBits);
-    }
-    // the rest of a step whose window entry e has been read: the long-code
-    // fix behind a wave-uniform branch (EOS or a code running past the end
-    // rejects, D3), the arena bytes, the window moved on c bits
-    __device__ __forceinline__ void step(uint32_t e, const QH_LDS uint32_t *src,
-                                         const QH_LDS uint16_t *s_sorted)
-    {
-        uint32_t c = ent_c(e), ns = ent_ns(e);
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(e < (1u << 24)) != 0, 0))
-        {
-            const bool lng = e < (1u << 24);
-            uint32_t L;
-            const uint32_t sym = long_code(W, s_sorted, &L);
-            const bool rej = lng & ((sym == 256) | (L > rem));
-            e = lng ? sym : e;
-            c = lng ? (rej ? 0u : L) : c;
-            ns = lng ? (rej ? 0u : 1u) : ns;
-            bad |= rej ? 1u : 0u;
-            rem = rej ? 0u : rem;
-        }
-        q[0] = (uint8_t) e;
-        q[1] = (uint8_t) (e >> 16);
-        q += ns;
-        rem -= c;
-        uint32_t tn;
-        const bool cross = __builtin_sub_overflow(t, c, &tn);
-        A = cross ? B : A;
-        B = cross ? nx : B;
-        t = tn & 31;
-        p += cross ? 1u : 0u;
-        nx = src[p];
-        W = __builtin_amdgcn_alignbit(A, B, t);
-        idx = win_addr(W, rem >= kWinBits);
-    }
-    // the last < kWinBits bits (decode_string_lds's one-pass epilogue)
-    __device__ __forceinline__ int tail(const QH_LDS uint32_t *s_win)
-    {
-        const bool live = !(bad || rem == 0);
-        const uint32_t w = W | (0xffffffffu >> (rem & 31));
-        const uint32_t e = s_win[w >> (32 - kWinBits)];
-        const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
-        const bool two = (ns == 2) & (ct <= rem);
-        const bool one = !two & (ns != 0) & (l0 <= rem);
-        const uint32_t c = two ? ct : (one ? l0 : 0u);
-        q[0] = (uint8_t) e;
-        q[1] = (uint8_t) (e >> 16);
-        q += live ? (two ? 2u : (one ? 1u : 0u)) : 0u;
-        const uint32_t r2 = rem - c;
-        const uint32_t inv = ~(w << (c & 31));
-        const bool pad_ok = r2 < 8 && (r2 == 0 || (inv >> ((32 - r2) & 31)) == 0);
-        bad |= (live & !pad_ok) ? 1u : 0u;
-        return bad ? -1 : (int) (q - slot);
-    }
-};
-
-// Two strings per lane, decoded together: both chains' window lookups are
-// issued before either is used, so the two dependent LDS round trips of a
-// step overlap (a chain with < kWinBits bits left reads the hold entry and
-// stands still).  The loop runs to the longer chain of the wave.
-__device__ __forceinline__ void
-decode_pair_lds(const QH_LDS uint32_t *src, uint32_t b0, uint32_t b1,
-                uint32_t b2, QH_LDS uint8_t *slot0, QH_LDS uint8_t *slot1,
-                const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
-                int *r0, int *r1)
-{
-    LdsChain x, y;
-    x.init(src, b0, b1, slot0);
-    y.init(src, b1, b2, slot1);
-    auto lds_at = [&](uint32_t a) -> uint32_t {
-        return *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + a);
-    };
-    if (__builtin_amdgcn_ballot_w64((x.rem >= kWinBits) | (y.rem >= kWinBits)))
-    do
-    {
-        const uint32_t ex = lds_at(x.idx);
-        const uint32_t ey = lds_at(y.idx);
-        x.step(ex, src, s_sorted);
-        y.step(ey, src, s_sorted);
-    } while (__builtin_amdgcn_ballot_w64((x.rem >= kWinBits) | (y.rem >= kWinBits)));
-    *r0 = x.tail(s_win);
-    *r1 = y.tail(s_win);
 }
 
 // byte-granular arena sink: two unconditional byte stores per step, the
@@ -790,61 +391,10 @@ struct ArenaEmit
     __device__ __forceinline__ void finish() { n = (uint32_t) (p - slot); }
     __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
     {
-#if QH_EMITCOND
-        if (nb)                              // exec-masked: held lanes skip
-#endif
-        {
-            p[0] = (uint8_t) val;
-            p[1] = (uint8_t) (val >> 16);
-        }
+        // (exec-masked for held lanes only: slower, profiles/r02_e)
+        p[0] = (uint8_t) val;
+        p[1] = (uint8_t) (val >> 16);
         p += nb;
-    }
-};
-
-// dword emitter (QH_PAIR): output bytes gathered in a register and stored
-// as aligned dwords into the lane's dword-aligned arena slot; the bytes of a
-// step are the entry's sym0 [7:0] and sym1 [23:16] (sym1 = 0 in a
-// one-symbol entry, so two steps' bytes combine with one shift-or)
-struct DwordEmit
-{
-    QH_LDS uint32_t *slot;
-    uint32_t w;                      // dwords stored
-    uint32_t pend;                   // pending bytes, low pb bits
-    uint32_t pb;                     // pending bits: 0, 8, 16 or 24
-    uint32_t n;                      // output bytes (after finish())
-    __device__ __forceinline__ static uint32_t bytes(uint32_t e)
-    {
-        return __builtin_amdgcn_perm(e, e, 0x0c0c0200u);   // sym1 : sym0
-    }
-    // append the low nbits (0..32, a multiple of 8) of x, no bits above
-    __device__ __forceinline__ void put(uint32_t x, uint32_t nbits)
-    {
-        const uint32_t lo = pend | (x << pb);
-        const uint32_t hi = (x >> 1) >> (31 - pb);   // x >> (32 - pb); 0 at pb 0
-        const uint32_t tot = pb + nbits;
-        const bool full = tot >= 32;
-        if (full)
-            slot[w] = lo;
-        w += full ? 1u : 0u;
-        pend = full ? hi : lo;
-        pb = tot & 31;
-    }
-    __device__ __forceinline__ void put2(uint32_t e1, uint32_t s1, uint32_t e2,
-                                         uint32_t s2)
-    {
-        put(bytes(e1) | (bytes(e2) << s1), s1 + s2);
-    }
-    // nb (0..2) symbols of entry (or symbol) val
-    __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
-    {
-        const uint32_t b = __builtin_amdgcn_ubfe(bytes(val), 0, 8 * nb);
-        put(b, 8 * nb);
-    }
-    __device__ __forceinline__ void finish()
-    {
-        if (pb)
-            slot[w] = pend;
-        n = 4 * w + pb / 8;
     }
 };
 
@@ -906,48 +456,6 @@ compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
     const uint32_t sb = s3 + h, r = sb & 3;
     const QH_LDS uint32_t *bw = sw + (sb >> 2);
     QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
-#if QH_COMPACT64
-    // (experiment) the body as 8-byte stores: one dword first when the
-    // dword-aligned destination is not 8-aligned, then four ds_write_b64 per
-    // trip of eight source dwords read together (a 64-bit store moves 3
-    // dwords through the LDS port, two 32-bit stores 4), a last odd dword
-    const uint32_t a = (nb != 0) & ((((uint32_t) (uintptr_t) dw) & 4) != 0);
-    const uint32_t m = nb - a, nq = m >> 1;
-    const QH_LDS uint32_t *bq = bw + a;
-    QH_LDS uint32_t *dq = dw + a;            // 8-byte aligned
-    const uint32_t w0 = bw[0];
-    uint32_t cur = bq[0];
-    uint32_t nw[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        nw[j] = bq[j + 1];
-    write_bytes(dstb, vh, h);
-    write_bytes(dstb + it, vt, nt);
-    if (a)
-        dw[0] = align_bytes(cur, w0, r);
-    for (uint32_t k = 0; k < nq; k += 4)
-    {
-        if (k)
-        {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                nw[j] = bq[2 * k + j + 1];
-        }
-        uint32_t v[8];
-        v[0] = align_bytes(nw[0], cur, r);
-#pragma unroll
-        for (int j = 1; j < 8; ++j)
-            v[j] = align_bytes(nw[j], nw[j - 1], r);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (k + j < nq)
-                *(QH_LDS uint64_t *) (dq + 2 * (k + j)) =
-                    (uint64_t) v[2 * j] | ((uint64_t) v[2 * j + 1] << 32);
-        cur = nw[7];
-    }
-    if (m & 1)
-        dq[2 * nq] = align_bytes(bq[2 * nq + 1], bq[2 * nq], r);
-#elif QH_COMPACT8
     // Eight dwords per trip, the trip's source words read together and the
     // last one carried into the next trip (reads past the string stay in
     // the wave's LDS region or past the allocation, where LDS reads 0).
@@ -976,25 +484,6 @@ compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
                 dw[k + j] = align_bytes(nw[j], nw[j - 1], r);
         cur = nw[7];
     }
-#else
-    write_bytes(dstb, vh, h);
-    write_bytes(dstb + it, vt, nt);
-    for (uint32_t k = 0; k < nb; k += 4)
-    {
-        const uint32_t w0 = bw[k];
-        const uint32_t w1 = bw[k + 1];
-        const uint32_t w2 = k + 1 < nb ? bw[k + 2] : 0u;
-        const uint32_t w3 = k + 2 < nb ? bw[k + 3] : 0u;
-        const uint32_t w4 = k + 3 < nb ? bw[k + 4] : 0u;
-        dw[k] = align_bytes(w1, w0, r);
-        if (k + 1 < nb)
-            dw[k + 1] = align_bytes(w2, w1, r);
-        if (k + 2 < nb)
-            dw[k + 2] = align_bytes(w3, w2, r);
-        if (k + 3 < nb)
-            dw[k + 3] = align_bytes(w4, w3, r);
-    }
-#endif
 }
 
 // A tile whose input or output does not fit the stage, coded eagerly:
@@ -1057,94 +546,6 @@ dec_slow_tile(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
     }
 }
 
-#if QH_DUAL
-// dec_slow_tile for two strings per lane (strings 2l and 2l + 1)
-__device__ __noinline__ void
-dec_slow_tile2(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
-               uint32_t slot0, uint32_t slot1, uint32_t sz0, Coord c,
-               uint32_t t, uint32_t cnt, TileOffs2 to, Span sp, uint32_t sz,
-               uint32_t st, uint8_t *out, uint32_t *out_off, uint8_t *status,
-               uint64_t n)
-{
-    const uint32_t lane = lane_id();
-    const bool v0 = 2 * lane < cnt, v1 = 2 * lane + 1 < cnt;
-    const uint32_t r0s = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
-    const uint32_t r1s = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
-    const uint32_t r1e = (uint32_t) ((uintptr_t) (in + to.o2) - sp.pa);
-    const DecGlb src{(const QH_GLB uint32_t *) sp.pa};
-    uint32_t z0 = sz0, z1 = sz - sz0;
-    uint32_t st0 = st & 0xff, st1 = st >> 8;
-    if (!sp.staged)
-    {
-        int a = 0, b = 0;
-        if (v0)
-        {
-            CountEmit em{0};
-            a = decode_string(src, 8 * r0s, 8 * r1s, sm->win, sm->sorted, em);
-        }
-        if (v1)
-        {
-            CountEmit em{0};
-            b = decode_string(src, 8 * r1s, 8 * r1e, sm->win, sm->sorted, em);
-        }
-        z0 = a < 0 ? 0u : (uint32_t) a;
-        z1 = b < 0 ? 0u : (uint32_t) b;
-        st0 = a < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
-        st1 = b < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
-    }
-    const uint32_t incl = wave_incl_scan(z0 + z1);
-    const uint32_t excl = incl - (z0 + z1);
-    const uint32_t total = read_lane(incl, 63);
-    LookBack lb;
-    lb.start(c, t, total);
-    lb.super_agg(c);
-    lb.poll(c);
-    const uint64_t base = lb.finish(c);
-    uint8_t *d0 = out + base + excl;
-    uint8_t *d1 = d0 + z0;
-    if (sp.staged)
-    {
-        const QH_LDS uint8_t *a0 = wv->arena + slot0;
-        const QH_LDS uint8_t *a1 = wv->arena + slot1;
-        for (uint32_t i = 0; i < z0; ++i)
-            ((QH_GLB uint8_t *) d0)[i] = a0[i];
-        for (uint32_t i = 0; i < z1; ++i)
-            ((QH_GLB uint8_t *) d1)[i] = a1[i];
-    }
-    else
-    {
-        if (v0 && st0 == QHUFF_DEC_OK && z0)
-        {
-            GlobalEmit em{d0, 0};
-            decode_string(src, 8 * r0s, 8 * r1s, sm->win, sm->sorted, em);
-        }
-        if (v1 && st1 == QHUFF_DEC_OK && z1)
-        {
-            GlobalEmit em{d1, 0};
-            decode_string(src, 8 * r1s, 8 * r1e, sm->win, sm->sorted, em);
-        }
-    }
-    const uint64_t s0 = (uint64_t) t * kDecTS;
-    if (v0)
-    {
-        ((QH_GLB uint32_t *) out_off)[s0 + 2 * lane] = (uint32_t) (base + excl);
-        ((QH_GLB uint8_t *) status)[s0 + 2 * lane] = (uint8_t) st0;
-    }
-    if (v1)
-    {
-        ((QH_GLB uint32_t *) out_off)[s0 + 2 * lane + 1] =
-            (uint32_t) (base + excl + z0);
-        ((QH_GLB uint8_t *) status)[s0 + 2 * lane + 1] = (uint8_t) st1;
-    }
-    if (t == c.n_tiles - 1 && lane == 0)
-    {
-        ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + total);
-        if (base + total > 0xffffffffull)        // offsets are 32-bit
-            raise_error(c, kErrRange);
-    }
-}
-#endif
-
 // the decode side of the wave pipeline (qhuff_pipeline.h)
 struct DecPolicy
 {
@@ -1152,23 +553,14 @@ struct DecPolicy
     static constexpr int kInCap = kDecInCap;
     static constexpr int kDepth = QH_DEPTH;       // pending tiles
     static constexpr int kOutCap = kDecStageCap;
-    static constexpr bool kPark = false;
     static constexpr int kNch = kDecNch;          // 16-byte chunks per lane
     static constexpr uint32_t kTS = kDecTS;       // strings per tile
-    static constexpr bool kPairs = kDual;         // two strings per lane
-#if QH_DUAL
-    using Offs = TileOffs2;
-#else
     using Offs = TileOffs;
-#endif
     const uint8_t *in;
     QH_LDS DecSmem *sm;
     QH_LDS DecWave *wv;
     uint32_t slot0;                  // this lane's arena slot (current tile)
-    uint32_t slot1;                  // (QH_DUAL) its second string's
-    uint32_t sz0;                    // (QH_DUAL) its first string's size
 
-    __device__ __forceinline__ uint32_t first_size() const { return sz0; }
     __device__ __forceinline__ void stage_in(const Chunks<kNch> &ch,
                                              const Span &sp, const Offs &)
     {
@@ -1179,79 +571,32 @@ struct DecPolicy
     {
         return wv->in;
     }
-    __device__ __forceinline__ QH_LDS uint32_t *park_buf() const
-    {
-        return nullptr;
-    }
     // staged tile: decode this lane's string into its arena slot
     __device__ __forceinline__ void codec(const Offs &to, uint32_t cnt,
                                           const Span &sp, uint32_t *sz,
                                           uint32_t *st)
     {
         const uint32_t lane = lane_id();
-#if QH_DUAL
-        // strings 2l and 2l + 1; lanes past the count decode empty strings
-        (void) cnt;
         const uint32_t A = to.first();
-        slot0 = 4 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
-        slot1 = 4 * lane + 2 + (uint32_t) ((8ull * (to.o1 - A)) / 5);
-        const uint32_t b0 = 8 * (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
-        const uint32_t b1 = 8 * (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
-        const uint32_t b2 = 8 * (uint32_t) ((uintptr_t) (in + to.o2) - sp.pa);
-        int r0, r1;
-        decode_pair_lds(wv->in, b0, b1, b2, wv->arena + slot0,
-                        wv->arena + slot1, sm->win, sm->sorted, &r0, &r1);
-        sz0 = r0 < 0 ? 0u : (uint32_t) r0;
-        *sz = sz0 + (r1 < 0 ? 0u : (uint32_t) r1);
-        *st = (r0 < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK)
-            | (r1 < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK) << 8;
-#else
-        const uint32_t A = to.first();
-#if QH_PAIR
-        slot0 = 4 * (lane + (uint32_t) ((2ull * (to.o0 - A)) / 5));
-#else
         slot0 = 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
-#endif
         int r = 0;
         if (lane < cnt)
         {
             const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
             const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
-#if QH_EXP == 1   // (timing experiment: no codec)
-            r = (int) (((re - rs) * 23) >> 4);
-#else
-#if QH_PAIR
-            DwordEmit em{(QH_LDS uint32_t *) (wv->arena + slot0), 0, 0, 0, 0};
-#else
             ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
-#endif
             r = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted,
                                   em);
-#endif
         }
         *sz = r < 0 ? 0u : (uint32_t) r;
         *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
-#endif
     }
     // arena -> the (dead) input stage, compacted
     __device__ __forceinline__ void emit(uint32_t excl, uint32_t sz, uint32_t)
     {
-#if QH_DUAL
-        if (sz0)
-            compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
-                           sz0);
-        if (sz - sz0)
-            compact_string(wv->arena + slot1,
-                           (QH_LDS uint8_t *) wv->in + excl + sz0, sz - sz0);
-#else
-#if QH_EXP == 2   // (timing experiment: no compaction)
-        if (0)
-#else
         if (sz)
-#endif
             compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
                            sz);
-#endif
     }
 
     __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
@@ -1260,13 +605,8 @@ struct DecPolicy
                                               uint32_t *out_off, uint8_t *status,
                                               uint64_t n)
     {
-#if QH_DUAL
-        dec_slow_tile2(in, sm, wv, slot0, slot1, sp.staged ? sz0 : 0u, c, t,
-                       cnt, to, sp, sz, st, out, out_off, status, n);
-#else
         dec_slow_tile(in, sm, wv, slot0, c, t, cnt, to, sp, sz, st, out,
                       out_off, status, n);
-#endif
     }
 };
 
@@ -1301,13 +641,7 @@ qhuff_decode_kernel(DecArgs a)
         {
             const int i = tid + r * 64 * kWaves;
             if (i < kWinSize / 4)
-            {
-#if QH_NSBYTE
-                const uint32_t m = 0x03ffffffu;      // drop [31:26]
-                v[r] = (u32x4){v[r].x & m, v[r].y & m, v[r].z & m, v[r].w & m};
-#endif
                 sw[i] = v[r];
-            }
         }
         if (tid < 257)
             sm->sorted[tid] = so;
@@ -1317,7 +651,7 @@ qhuff_decode_kernel(DecArgs a)
     }
     __syncthreads();                 // the only workgroup barrier
     prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
-    DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0, 0, 0};
+    DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
     uint32_t k0, k1;
     wave_tickets(tk, &sm->tk, &k0, &k1);
     tile_pipeline(pol, a.c, tk, k0, k1, a.in, a.in_off,

@@ -10,11 +10,12 @@
 // stores.  No workgroup barrier is taken inside the tile loop.
 //
 // Every global round trip is kept off a wave's critical path (see
-// qhuff_pipeline.h): tiles are assigned statically (tile k of wave g is
-// g + k * W), offsets are loaded two tiles ahead and input one tile ahead,
-// and a tile's look-back and stores are deferred until after the next
-// tile's codec -- its output waits in registers -- so polls find their
-// predecessors published and no wait drains freshly issued stores.
+// qhuff_pipeline.h): tiles come from in-order tickets claimed two
+// iterations ahead (Tickets), offsets are loaded two tiles ahead and input
+// one tile ahead, and a tile's look-back and stores are deferred until
+// after the next tile's codec -- its output waits in registers -- so polls
+// find their predecessors published and no wait drains freshly issued
+// stores.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -31,12 +32,6 @@ struct __attribute__((packed, aligned(1))) U1 { uint32_t v; };
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWT = 64;                     // strings per wave tile
-// tile offsets by one vector load + a DPP shift + a uniform load of the
-// entry after the tile: slower (enc 64.8 vs 63.4, dec 67.9 vs 66.7 us,
-// profiles/r02_o/ab_off1.txt); off
-#ifndef QH_OFF1
-#define QH_OFF1 0
-#endif
 #ifndef QH_WAVES
 #define QH_WAVES 12
 #endif
@@ -61,15 +56,10 @@ constexpr uint64_t kAccMask = kAccOne - 1;
 // 'dequeue'), and with 16 accumulators per line every running super tile's
 // adds queued on a handful of lines -- the returned add then cost ~3.5k
 // cycles of each tile's poll wait (profiles/r02_c/phases_*.txt)
-#ifndef QH_ACC_STRIDE
-#define QH_ACC_STRIDE 32
-#endif
-constexpr uint32_t kAccStride = QH_ACC_STRIDE;
-// tile flags kFlagStride u64 apart (1: dense, a poll window is 4 lines)
-#ifndef QH_FLAG_STRIDE
-#define QH_FLAG_STRIDE 1
-#endif
-constexpr uint32_t kFlagStride = QH_FLAG_STRIDE;
+constexpr uint32_t kAccStride = 32;
+// tile flags kFlagStride u64 apart (1: dense, a poll window is 4 lines;
+// 4 and 16 were equal / 3 % slower, profiles/r02_h/ab_tile_flag_stride.txt)
+constexpr uint32_t kFlagStride = 1;
 
 // error bits reported through Coord::err
 constexpr uint32_t kErrSpin = 1;            // look-back spin limit hit
@@ -80,11 +70,9 @@ constexpr uint32_t kErrRange = 2;           // output offsets passed 2^32
 // claims/us on MI355X, MI355X_MICROARCH.md 'dequeue').  Group g (blocks with
 // blockIdx % G == g) claims tiles g, g + G, g + 2G, ... in order, so every
 // tile a look-back waits on is held by a wave that is running: no
-// co-residency assumption.
-#ifndef QH_TICK_GROUPS
-#define QH_TICK_GROUPS 8
-#endif
-constexpr uint32_t kTickGroups = QH_TICK_GROUPS;
+// co-residency assumption.  (12 groups, one per wave of a workgroup, was
+// 4 % slower: profiles/r02_r/ab_tick_groups12.txt)
+constexpr uint32_t kTickGroups = 8;
 // each counter on its own 256-byte span (u32 stride): atomics to one line
 // serialise in one L2 channel, and every other access of that channel waits
 constexpr uint32_t kTickStride = 64;
@@ -356,16 +344,9 @@ struct TileOffs
     {
         const uint32_t lane = lane_id();
         o0 = in_off[s0 + (lane < cnt ? lane : cnt)];
-#if QH_OFF1
-        // o1 is the next lane's o0 (one vector load, not two), lane 63's
-        // from a scalar load of the entry after the tile
-        const uint32_t last = in_off[s0 + cnt];
-        const uint32_t nx = (uint32_t) __builtin_amdgcn_update_dpp(
-            0, (int) o0, 0x130, 0xf, 0xf, false);   // wave_shl:1
-        o1 = lane == 63 ? last : nx;
-#else
+        // (o1 as the next lane's o0 by a DPP shift + one uniform load was
+        // slower: enc 64.8 vs 63.4, dec 67.9 vs 66.7 us, r02_o/ab_off1.txt)
         o1 = in_off[s0 + (lane + 1 < cnt ? lane + 1 : cnt)];
-#endif
     }
     __device__ __forceinline__ uint32_t first() const { return read_lane(o0, 0); }
     __device__ __forceinline__ uint32_t last() const { return read_lane(o1, 63); }
@@ -559,9 +540,6 @@ struct LookBack
     // publishes its inclusive one
     __device__ __forceinline__ uint64_t finish(const Coord &c)
     {
-#if QH_EXP == 3   // (timing experiment: no look-back)
-        return 0;
-#endif
         const uint32_t lane = lane_id();
         const uint32_t f0 = s * kSuper;
         const uint32_t nq = tile - f0;               // earlier tiles in super
@@ -657,13 +635,6 @@ struct TileOut
         for (int j = 0; j < NCH; ++j)
             o[j] = ((const QH_LDS u32x4 *) stage)[lane + 64 * j];
     }
-    __device__ __forceinline__ void park(QH_LDS uint32_t *hold) const
-    {
-        const uint32_t lane = lane_id();
-#pragma unroll
-        for (int j = 0; j < NCH; ++j)
-            ((QH_LDS u32x4 *) hold)[lane + 64 * j] = o[j];
-    }
 
     // Global stores of the tile's `total` bytes at dst (any alignment: the
     // ROCm driver runs gfx9 in unaligned-access mode, and the 16-byte stores
@@ -672,9 +643,6 @@ struct TileOut
     // writes its whole dwords, then its last 0-3 bytes.
     __device__ __forceinline__ void store(uint8_t *dst, uint32_t total) const
     {
-#if QH_EXP == 4   // (timing experiment: 16-byte aligned stores, wrong bytes)
-        dst = (uint8_t *) ((uintptr_t) dst & ~(uintptr_t) 15);
-#endif
         const uint32_t lane = lane_id();
         const uint32_t nfull = total >> 4, rem = total & 15;
         // the lane's byte offset comes out of an opaque instruction here, at

@@ -31,24 +31,11 @@
 // (global reads / per-lane global writes).
 #include "qhuff_pipeline.h"
 
+// pending tiles: at 3 the tiles' outputs in registers spill (enc 91 vs 75
+// us); the oldest parked in LDS instead still spilled 5 VGPRs in the dense
+// pass (72.8 vs 65.5 us, profiles/r02_h)
 #ifndef QH_ENC_DEPTH
 #define QH_ENC_DEPTH 2
-#endif
-// QH_PARK=1: the oldest of the pending tiles waits in an LDS park buffer
-// instead of registers.  Measured with QH_ENC_DEPTH=3 (three tiles' outputs
-// in registers spill): look-back re-polls 0.7 -> 0.04 per tile, but 5 VGPRs
-// still spill in the dense pass and the park round trip costs -- enc 72.8 vs
-// 65.5 us at depth 2 (profiles/r02_h).  Off.
-#ifndef QH_PARK
-#define QH_PARK 0
-#endif
-// the dense pass's three stage rows read up front (one LDS round trip):
-// enc 66.1 vs 65.4 us, not kept (profiles/r02_l/ab_rows_first.txt)
-#ifndef QH_COPY4
-#define QH_COPY4 1
-#endif
-#ifndef QH_ROWS_FIRST
-#define QH_ROWS_FIRST 0
 #endif
 
 namespace qhuff {
@@ -65,9 +52,6 @@ struct EncWave                                // one wave's private LDS region
     alignas(16) uint32_t dense[kDenseWords];    // codes back to back, MSB first
     alignas(16) uint32_t out[kEncOutCap / 4];   // byte code lengths until emit
     uint32_t s0[kSpanChunks];                   // dense offset of each chunk
-#if QH_PARK
-    alignas(16) uint32_t park[kStageCap / 4];   // oldest pending tile's output
-#endif
 };
 
 struct EncSmem
@@ -490,18 +474,8 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
     wave_sync();
     QH_LDS u32x4 *lens4 = (QH_LDS u32x4 *) wv->out;
     uint32_t carry = 0, big = 0;
-#if QH_ROWS_FIRST
-    // the rows' stage chunks read together (one LDS round trip, not one per
-    // row behind the previous row's dense ORs)
-    u32x4 wrow[kChunks];
-#pragma unroll
-    for (int k = 0; k < kChunks; ++k)
-    {
-        const uint32_t c = lane + 64u * k;
-        const uint32_t last = n16 ? n16 - 1 : 0;
-        wrow[k] = ((const QH_LDS u32x4 *) wv->in)[c < last ? c : last];
-    }
-#endif
+    // (the three rows' stage chunks read up front, one LDS round trip: enc
+    // 66.1 vs 65.4 us, profiles/r02_l/ab_rows_first.txt)
 #pragma unroll
     for (int k = 0; k < kChunks; ++k)
     {
@@ -509,12 +483,8 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
         // lets the rows' lookups overlap; chunks past the span read its last
         // staged chunk again, coded past its end and never read
         const uint32_t c = lane + 64u * k;
-#if QH_ROWS_FIRST
-        const u32x4 w = wrow[k];
-#else
         const uint32_t last = n16 ? n16 - 1 : 0;
         const u32x4 w = ((const QH_LDS u32x4 *) wv->in)[c < last ? c : last];
-#endif
         const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
         uint32_t m[16];
 #pragma unroll
@@ -600,7 +570,6 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
     const uint32_t e = d + nb;
     const uint32_t w0 = d >> 5, wl = (e - 1) >> 5, od = d & 31;
     const uint32_t tailm = 0xffffffffu << (31 - ((e - 1) & 31));
-#if QH_COPY4
     // Every read of the first word, the first trip and the last word is
     // issued before any write (a wave's LDS operations run in order, so a
     // read behind a write waits for it): a string of up to 6 output words
@@ -651,34 +620,6 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
     }
     __hip_atomic_fetch_or(&st[wl], bswap32(win(la, lb) & tailm),
                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-    {
-        const uint32_t q = s >> 5, os = s & 31;
-        const uint32_t a = dense[q], b = dense[q + 1];
-        uint32_t v = os ? __builtin_amdgcn_alignbit(a, b, 32 - os) : a;
-        v >>= od;
-        if (w0 == wl)
-            v &= tailm;
-        __hip_atomic_fetch_or(&st[w0], bswap32(v), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    const uint32_t x1 = s - od + 32, sh = x1 & 31;
-    uint32_t q = x1 >> 5;
-    uint32_t cur = dense[q];
-#pragma unroll 2
-    for (uint32_t w = w0 + 1; w <= wl; ++w)
-    {
-        const uint32_t nxt = dense[q + 1];
-        const uint32_t v = sh ? __builtin_amdgcn_alignbit(cur, nxt, 32 - sh) : cur;
-        if (w == wl)
-            __hip_atomic_fetch_or(&st[w], bswap32(v & tailm), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-        else
-            st[w] = bswap32(v);
-        cur = nxt;
-        ++q;
-    }
-#endif
 }
 
 // one string from the dense stream: framing, payload bits [s, s + bits),
@@ -767,12 +708,9 @@ struct EncPolicy
     static constexpr int kInCap = kEncInCap;
     static constexpr int kDepth = QH_ENC_DEPTH;       // pending tiles
     static constexpr int kOutCap = kEncOutCap;
-    static constexpr bool kPark = QH_PARK;
     static constexpr int kNch = kChunks;          // 16-byte chunks per lane
     static constexpr uint32_t kTS = kWT;          // strings per tile
-    static constexpr bool kPairs = false;         // one string per lane
     using Offs = TileOffs;
-    __device__ __forceinline__ uint32_t first_size() const { return 0; }
     const uint8_t *in;
     uint32_t mode;                   // 0 payload, 3/5/7 literal prefix bits
     QH_LDS EncSmem *sm;
@@ -798,17 +736,6 @@ struct EncPolicy
     {
         return wv->out;
     }
-#if QH_PARK
-    __device__ __forceinline__ QH_LDS uint32_t *park_buf() const
-    {
-        return wv->park;
-    }
-#else
-    __device__ __forceinline__ QH_LDS uint32_t *park_buf() const
-    {
-        return nullptr;
-    }
-#endif
     // staged tile: size this lane's string (E1, and the E3 choice)
     __device__ __forceinline__ void codec(const TileOffs &to, uint32_t cnt,
                                           const Span &sp, uint32_t *sz,

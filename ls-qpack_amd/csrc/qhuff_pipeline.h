@@ -51,12 +51,7 @@ struct Pending
     bool valid;
     uint32_t tile, cnt, total;
     uint32_t excl;                   // this lane's tile-local output offset
-    uint32_t stat;                   // this lane's status byte (two strings
-                                     // per lane: [7:0], [15:8], and the
-                                     // first one's size [31:16])
-#if QH_EXP == 3
-    uint32_t fake_base;
-#endif
+    uint32_t stat;                   // this lane's status byte
     LookBack lb;
 };
 
@@ -66,35 +61,13 @@ __device__ __forceinline__ void
 flush_tile(const Coord &c, Pending &d, const TileOut<P::kNch> &o, uint8_t *out,
            uint32_t *out_off, uint8_t *status, uint64_t n, uint32_t it = ~0u)
 {
-#if QH_EXP == 3   // (timing experiment: no look-back; base = input offset)
-    const uint64_t base = d.fake_base;
-#else
     const uint64_t base = d.lb.finish(c);
-#endif
     prof_stamp(c, it, 7);
     prof_value(c, it, 8, d.lb.spins_seen);
     o.store(out + base, d.total);
     const uint32_t lane = lane_id();
     const uint64_t s0 = (uint64_t) d.tile * P::kTS;
-    if (P::kPairs)
-    {
-        // lane l: strings 2l and 2l + 1 of the tile
-        const uint32_t i0 = 2 * lane;
-        if (i0 < d.cnt)
-        {
-            ((QH_GLB uint32_t *) out_off)[s0 + i0] = (uint32_t) (base + d.excl);
-            if (P::kStatus)
-                ((QH_GLB uint8_t *) status)[s0 + i0] = (uint8_t) d.stat;
-        }
-        if (i0 + 1 < d.cnt)
-        {
-            ((QH_GLB uint32_t *) out_off)[s0 + i0 + 1] =
-                (uint32_t) (base + d.excl + (d.stat >> 16));
-            if (P::kStatus)
-                ((QH_GLB uint8_t *) status)[s0 + i0 + 1] = (uint8_t) (d.stat >> 8);
-        }
-    }
-    else if (lane < d.cnt)
+    if (lane < d.cnt)
     {
         ((QH_GLB uint32_t *) out_off)[s0 + lane] = (uint32_t) (base + d.excl);
         if (P::kStatus)
@@ -115,16 +88,6 @@ wait_vm_all()
 {
     __builtin_amdgcn_s_waitcnt(0x0f70);
 }
-
-#ifndef QH_WAIT
-#define QH_WAIT 1
-#endif
-#ifndef QH_TOPWAIT
-#define QH_TOPWAIT 1
-#endif
-#ifndef QH_EXP
-#define QH_EXP 0
-#endif
 
 // The kernel prologue claims the first two tickets of every wave of the
 // workgroup: lanes 0..kTickGroups-1 of the first wave each take one group's
@@ -238,25 +201,13 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     constexpr int D = P::kDepth;
     Pending pend[D];
     TileOut<P::kNch> outs[D];
-    // resolve + store pending tile i (compile-time i); with P::kPark the
-    // oldest one's output comes back from the park buffer first
+    // resolve + store pending tile i (compile-time i)
     auto flush_at = [&](int i, uint32_t itn) {
-        if (P::kPark && i == 0)
-        {
-            TileOut<P::kNch> o;
-            o.gather(pol.park_buf());
-            flush_tile<P>(c, pend[0], o, out, out_off, status, n, itn);
-        }
-        else
-            flush_tile<P>(c, pend[i], outs[i], out, out_off, status, n, itn);
+        flush_tile<P>(c, pend[i], outs[i], out, out_off, status, n, itn);
     };
 #pragma unroll
     for (int i = 0; i < D; ++i)
         pend[i].valid = false;
-    // the prologue's loads, drained here: every path into the loop top then
-    // has nothing outstanding that the top reads (see the top)
-    if (!QH_TOPWAIT)
-        wait_vm_all();
     uint32_t it = 0;
     for (;; ++it)
     {
@@ -265,13 +216,12 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         // top: t's input, offsets and ticket were issued a codec ago and have
         // landed at the last iteration's poll wait; what is still in flight
         // here is that iteration's flush (stores, flag store, super publish),
-        // which nothing below reads.  The wait is kept (QH_TOPWAIT=1): without
-        // it (prologue loads drained before the loop instead) the per-tile
-        // top wait fell from 1.8k to 0.3k cycles but the kernels did not get
-        // faster (enc 65.6 / dec 68.7 vs 65.3 / 68.3 us, interleaved A/B,
-        // profiles/r02_g) -- the waves then wait longer in their look-backs.
-        if (QH_TOPWAIT)
-            wait_vm_all();
+        // which nothing below reads.  The wait is kept: without it (prologue
+        // loads drained before the loop instead) the per-tile top wait fell
+        // from 1.8k to 0.3k cycles but the kernels did not get faster (enc
+        // 65.6 / dec 68.7 vs 65.3 / 68.3 us, interleaved A/B, profiles/r02_g)
+        // -- the waves then wait longer in their look-backs.
+        wait_vm_all();
         prof_stamp(c, it, 1);
         if (sp_cur.staged)
             pol.stage_in(ch, sp_cur, o_cur);
@@ -285,7 +235,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         const uint32_t tz = clamp(tnn);
         o_nn.load(in_off, (uint64_t) tz * TS, cnt_of(tz));
         kq = tnn < nt ? tk.claim(c) : kNone;
-        if (pend[0].valid && QH_EXP != 3)
+        if (pend[0].valid)
             pend[0].lb.poll(c);
         prof_stamp(c, it, 2);
 
@@ -315,14 +265,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
             cur.total = total;
             cur.excl = excl;
             cur.stat = st;
-            if constexpr (P::kPairs)
-                cur.stat = st | pol.first_size() << 16;
-#if QH_EXP == 3
-            cur.lb.tile = t;
-            cur.fake_base = o_cur.first();
-#else
             cur.lb.start(c, t, total);
-#endif
             wave_sync();
             pol.emit(excl, sz, total);
             wave_sync();
@@ -336,14 +279,13 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
 #endif
 
         // the polls (a codec and an emit ago); resolve + store the oldest
-        if (QH_WAIT == 1)
-            wait_vm_all();
+        wait_vm_all();
         prof_stamp(c, it, 4);
         // t's add has returned with the polls: publish its super tile's
         // aggregate if that add completed it -- here, an emit after the add,
         // not at the next iteration's top (look-backs of later super tiles
         // wait on it: encode re-polled the super windows on 1 tile in 3)
-        if (cur.valid && QH_EXP != 3)
+        if (cur.valid)
             cur.lb.super_agg(c);
         if (pend[0].valid)
             flush_at(0, it);
@@ -354,14 +296,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
             outs[i] = outs[i + 1];
         }
         pend[D - 1] = cur;
-        // P::kPark: the oldest pending tile waits in the wave's LDS park
-        // buffer, not in registers (after the flush above has read the
-        // buffer: a wave's LDS operations execute in order)
-        if (P::kPark && pend[0].valid)
-        {
-            wave_sync();
-            outs[0].park(pol.park_buf());
-        }
         prof_stamp(c, it, 5);
 
         if (fast)
