@@ -57,7 +57,23 @@ static_assert(kDecInCap % 16 == 0 && kDecInCap <= kDecStageCap, "input cap");
 // byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
 // most 8/5 of its input, plus one byte written past the end by the
 // two-byte emitter
-constexpr int kArenaBytes = 2 * kDecTS + 8 * kDecInCap / 5 + QH_ARENA_SLACK;
+constexpr int kVarArenaBytes = 2 * kDecTS + 8 * kDecInCap / 5 + QH_ARENA_SLACK;
+// Tiles whose strings are all short enough use a fixed-stride arena
+// instead: lane l's slot at kFixStride * l.  The stride is an odd number of
+// dwords, so the byte stores of lanes that have emitted about as many
+// bytes fall on distinct banks (with slots placed by input offset the 64
+// stores of a step land on random banks: the stores were two thirds of the
+// step loop's LDS bank-conflict cycles, profiles/r03_b).  A string of at
+// most kFixMaxLen Huffman bytes decodes to at most floor(8 * len / 5) bytes
+// and the emitter writes one past its end.
+#ifndef QH_FIX_STRIDE
+#define QH_FIX_STRIDE 108
+#endif
+constexpr uint32_t kFixStride = QH_FIX_STRIDE;
+static_assert(kFixStride % 8 == 4, "an odd number of dwords");
+constexpr uint32_t kFixMaxLen = (5 * (kFixStride - 1)) / 8;
+constexpr int kArenaBytes = kVarArenaBytes > (int) (64 * kFixStride)
+                          ? kVarArenaBytes : (int) (64 * kFixStride);
 
 struct DecWave                       // one wave's private LDS region
 {
@@ -578,7 +594,10 @@ struct DecPolicy
     {
         const uint32_t lane = lane_id();
         const uint32_t A = to.first();
-        slot0 = 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
+        const bool fixed = !__builtin_amdgcn_ballot_w64(
+            (lane < cnt) & (to.o1 - to.o0 > kFixMaxLen));
+        slot0 = fixed ? kFixStride * lane
+                      : 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
         int r = 0;
         if (lane < cnt)
         {
