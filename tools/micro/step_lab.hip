@@ -66,6 +66,25 @@ struct U16Emit
     }
 };
 
+// the window entry itself, one ds_write_addtid_b32 per step into a
+// step-major arena (address M0 + 4 * lane, no address VGPR; M0 moves on
+// 256 B per step, wrapping in 4 KB: timing only, the bytes are not kept)
+struct AddtidEmit
+{
+    uint32_t base;                   // wave's arena byte address (uniform)
+    uint32_t step;                   // uniform step counter
+    uint32_t n;
+    __device__ __forceinline__ void finish() {}
+    __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
+    {
+        const uint32_t m0 = base + ((step & 15u) << 8);
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tds_write_addtid_b32 %0"
+                     : : "v"(val), "s"(m0) : "m0", "memory");
+        ++step;
+        n += nb;
+    }
+};
+
 struct MbOut { unsigned long long cyc, steps, sum; };
 
 template <int W, int MODE>
@@ -158,6 +177,65 @@ lab(DecArgs a, int reps, MbOut *res)
     }
 }
 
+// MODE 11 layout: the step-major arenas first (M0[15:0] addresses the
+// first 64 KB only), then the tables and the input stages
+template <int W>
+struct AddtidSmem
+{
+    uint32_t arena[W][1024];                 // 16 steps x 64 lanes x 4 B
+    uint32_t win[kWinSize + 4];
+    uint16_t sorted[257];
+    alignas(16) uint32_t in[W][kDecStageCap / 4];
+};
+
+template <int W>
+__global__ __launch_bounds__(64 * W) void
+lab_addtid(DecArgs a, int reps, MbOut *res)
+{
+    __shared__ AddtidSmem<W> smem;
+    QH_LDS AddtidSmem<W> *sm = (QH_LDS AddtidSmem<W> *) &smem;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kWinSize; i += 64 * W)
+        sm->win[i] = a.win[i];
+    if (tid < 257)
+        sm->sorted[tid] = a.sorted[tid];
+    if (tid == 0)
+        sm->win[kHoldIdx] = kHoldEntry;
+    __syncthreads();
+    const uint32_t w = tid >> 6;
+    const uint32_t gid = blockIdx.x * W + w, lane = lane_id();
+    const uint32_t t = gid % a.c.n_tiles;
+    TileOffs to;
+    to.load((const QH_GLB uint32_t *) a.in_off, (uint64_t) t * kWT, kWT);
+    const Span sp = tile_span(a.in, to.first(), to.last(), kStageCap);
+    Chunks<kChunks> ch;
+    ch.load(sp);
+    ch.store<true>((QH_LDS u32x4 *) sm->in[w], sp.n16);
+    wave_sync();
+    const uint32_t rs = (uint32_t) ((uintptr_t) (a.in + to.o0) - sp.pa);
+    const uint32_t re = (uint32_t) ((uintptr_t) (a.in + to.o1) - sp.pa);
+    const uint32_t base = (uint32_t) (uintptr_t) &sm->arena[w][0];
+    unsigned long long c0 = 0, sum = 0;
+    for (int r = 0; r < reps; ++r)
+    {
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        AddtidEmit em{(uint32_t) __builtin_amdgcn_readfirstlane((int) base), 0, 0};
+        int n = decode_string_lds(sm->in[w], 8 * rs, 8 * re, sm->win,
+                                  sm->sorted, em);
+        sum += read_lane((uint32_t) n, 63);
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        c0 += t1 - t0;
+        wave_sync();
+    }
+    const uint32_t bits = wave_max(8 * (re - rs));
+    if (lane == 0)
+    {
+        res[gid].cyc = c0 / reps;
+        res[gid].steps = bits;
+        res[gid].sum = sum;
+    }
+}
+
 static void synth(uint32_t n, std::vector<uint8_t> &data, std::vector<uint32_t> &off)
 {
     const char *alpha = "abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, ";
@@ -201,6 +279,28 @@ static void henc(const HostTables &t, const std::vector<uint8_t> &d,
     ho[n] = h.size();
 }
 
+template <int W>
+static void run_addtid(const char *tag, const DecArgs &a, int reps)
+{
+    const int blocks = 256, nw = blocks * W;
+    MbOut *d;
+    hipMalloc(&d, sizeof(MbOut) * nw);
+    for (int rep = 0; rep < 2; ++rep)
+        hipLaunchKernelGGL((lab_addtid<W>), dim3(blocks), dim3(64 * W), 0, 0,
+                           a, reps, d);
+    hipDeviceSynchronize();
+    std::vector<MbOut> h(nw);
+    hipMemcpy(h.data(), d, sizeof(MbOut) * nw, hipMemcpyDeviceToHost);
+    double cyc = 0, bits = 0;
+    for (auto &x : h) { cyc += x.cyc; bits += x.steps; }
+    cyc /= nw;
+    bits /= nw;
+    printf("%-14s %2d waves/CU: %7.0f cycles/tile/wave  %5.0f cycles per "
+           "step (max string %4.0f bits)\n", tag, W, cyc, cyc / (bits / 11.6),
+           bits);
+    hipFree(d);
+}
+
 template <int W, int MODE>
 static void run(const char *tag, const DecArgs &a, int reps)
 {
@@ -226,6 +326,7 @@ static void run(const char *tag, const DecArgs &a, int reps)
 
 int main(int argc, char **argv)
 {
+    setvbuf(stdout, NULL, _IOLBF, 0);
     const uint32_t n = 1 << 20;
     std::vector<uint8_t> data, hd;
     std::vector<uint32_t> off, ho;
@@ -267,6 +368,9 @@ int main(int argc, char **argv)
     run<12, 4>("fixed 84", a, reps);
     run<12, 5>("fixed 76", a, reps);
     run<12, 6>("fixed 68", a, reps);
+    run_addtid<1>("addtid u32", a, reps);
+    run_addtid<8>("addtid u32", a, reps);
+    run_addtid<12>("addtid u32", a, reps);
     run<1, 7>("u16 unaligned", a, reps);
     run<12, 7>("u16 unaligned", a, reps);
     run<12, 8>("u16 fixed 84", a, reps);
