@@ -98,6 +98,8 @@ def report(tag, p):
         print("  poll wait split: older ops mean %.0f p90 %.0f | own start "
               "(aggregate store + super add) mean %.0f p90 %.0f"
               % (a.mean(), np.percentile(a, 90), b.mean(), np.percentile(b, 90)))
+    if os.environ.get("SLOW"):
+        slow_report(p, live)
     if not os.environ.get("TIMELINE"):
         return
     # timeline: start of iterations relative to the first stamp (s_memtime
@@ -114,6 +116,43 @@ def report(tag, p):
         print("  iter %2d: waves %5d  start p50 %8.0f max %8.0f   end p50 %8.0f max %8.0f"
               % (it, ok.sum(), np.median(s), s.max(),
                  np.median(e) if e.size else 0, e.max() if e.size else 0))
+
+
+def slow_report(p, live):
+    """Which waves are slow: wall time (s_memrealtime, 10 ns) per iteration
+    over iterations 0..3 of each wave, grouped by XCD (block % 8), by the
+    wave's index in its workgroup and by its age rank on its SIMD (w >> 2)."""
+    W = 12
+    ok = live[:, 4]
+    rows = np.nonzero(ok)[0]
+    per = (p[rows, 4, 11] - p[rows, 0, 11]) * 10.0 / 4        # ns/iteration
+    blk, w = rows // W, rows % W
+    print("  per-iteration wall time (ns): mean %.0f p10 %.0f p50 %.0f p90 %.0f max %.0f"
+          % (per.mean(), np.percentile(per, 10), np.median(per),
+             np.percentile(per, 90), per.max()))
+    for name, key, n in (("XCD (block % 8)", blk % 8, 8),
+                         ("wave in workgroup", w, W),
+                         ("age rank on SIMD (w >> 2)", w >> 2, 3)):
+        means = [per[key == k].mean() for k in range(n)]
+        print("  by %-26s %s" % (name, " ".join("%.0f" % m for m in means)))
+    # each wave's end: its last iteration's start (realtime) plus that
+    # iteration's length in cycles at the shader clock (~2.2 GHz)
+    nit = live.sum(axis=1)
+    allw = np.nonzero(live[:, 0])[0]
+    last = nit[allw] - 1
+    r0 = p[allw, 0, 11].min()
+    end_us = ((p[allw, last, 11] - r0) * 0.01
+              + (p[allw, last, 6] - p[allw, last, 0]) / 2200.0)
+    wa = (allw % W) >> 2
+    print("  wave end (us after the first start): p50 %.2f p90 %.2f max %.2f"
+          " | by age rank max %s | tiles per wave by age rank %s"
+          % (np.median(end_us), np.percentile(end_us, 90), end_us.max(),
+             " ".join("%.2f" % end_us[wa == k].max() for k in range(3)),
+             " ".join("%.2f" % nit[allw][wa == k].mean() for k in range(3))))
+    cu = np.array([per[blk == b].mean() for b in np.unique(blk)])
+    print("  by CU (block): mean %.0f sd %.0f min %.0f max %.0f | within-CU sd "
+          "%.0f" % (cu.mean(), cu.std(), cu.min(), cu.max(),
+                    np.mean([per[blk == b].std() for b in np.unique(blk)])))
 
 
 def main():
