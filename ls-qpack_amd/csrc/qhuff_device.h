@@ -446,7 +446,9 @@ struct LookBack
     uint32_t total;
     uint64_t acc_old;            // returned by the super accumulator add (lane 0)
     uint64_t ft, fs, fs1;        // polled tile flags, super flags back 0 / 1
+#ifdef QHUFF_PROFILE
     uint32_t spins_seen;         // re-polls of the last finish() (profiling)
+#endif
 
     __device__ __forceinline__ static uint64_t ep(const Coord &c)
     {
@@ -609,7 +611,12 @@ struct LookBack
                                 ? c.n_tiles - f0 : (uint32_t) kSuper;
         if (tile == f0 + in_super - 1)
             publish_super(c, kFlagInc, excl + total);
+#ifdef QHUFF_PROFILE
         spins_seen = spins1 | ((spins - spins1) << 12) | (extra << 24);
+#else
+        (void) spins1;
+        (void) extra;
+#endif
         return excl;
     }
 };

@@ -33,7 +33,9 @@
 
 // pending tiles: at 3 the tiles' outputs in registers spill (enc 91 vs 75
 // us); the oldest parked in LDS instead still spilled 5 VGPRs in the dense
-// pass (72.8 vs 65.5 us, profiles/r02_h)
+// pass (72.8 vs 65.5 us, profiles/r02_h); round 3, with the pending state
+// slimmed and the next tile's loads issued after the dense pass, 2 VGPRs
+// still spill: 68.3 vs 63.0 us (profiles/r03_i)
 #ifndef QH_ENC_DEPTH
 #define QH_ENC_DEPTH 2
 #endif

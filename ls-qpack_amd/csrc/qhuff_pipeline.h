@@ -49,10 +49,9 @@ constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: chunk registers / stage
 struct Pending
 {
     bool valid;
-    uint32_t tile, cnt, total;
     uint32_t excl;                   // this lane's tile-local output offset
     uint32_t stat;                   // this lane's status byte
-    LookBack lb;
+    LookBack lb;                     // (its tile and total: lb.tile, lb.total)
 };
 
 // resolve a pending tile's base and store it from `o` (every lane)
@@ -63,20 +62,24 @@ flush_tile(const Coord &c, Pending &d, const TileOut<P::kNch> &o, uint8_t *out,
 {
     const uint64_t base = d.lb.finish(c);
     prof_stamp(c, it, 7);
+#ifdef QHUFF_PROFILE
     prof_value(c, it, 8, d.lb.spins_seen);
-    o.store(out + base, d.total);
+#endif
+    const uint32_t tile = d.lb.tile, total = d.lb.total;
+    o.store(out + base, total);
     const uint32_t lane = lane_id();
-    const uint64_t s0 = (uint64_t) d.tile * P::kTS;
-    if (lane < d.cnt)
+    const uint64_t s0 = (uint64_t) tile * P::kTS;
+    const uint32_t cnt = (uint32_t) min((uint64_t) P::kTS, n - s0);
+    if (lane < cnt)
     {
         ((QH_GLB uint32_t *) out_off)[s0 + lane] = (uint32_t) (base + d.excl);
         if (P::kStatus)
             ((QH_GLB uint8_t *) status)[s0 + lane] = (uint8_t) d.stat;
     }
-    if (d.tile == c.n_tiles - 1 && lane == 0)
+    if (tile == c.n_tiles - 1 && lane == 0)
     {
-        ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + d.total);
-        if (base + d.total > 0xffffffffull)      // offsets are 32-bit
+        ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + total);
+        if (base + total > 0xffffffffull)        // offsets are 32-bit
             raise_error(c, kErrRange);
     }
     d.valid = false;
@@ -260,9 +263,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         {
             // publish t's aggregate, pack t into the LDS out stage
             cur.valid = true;
-            cur.tile = t;
-            cur.cnt = cnt;
-            cur.total = total;
             cur.excl = excl;
             cur.stat = st;
             cur.lb.start(c, t, total);
