@@ -327,13 +327,17 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         sp_cur = sp_nxt;
     }
     wait_vm_all();
+    // the drain: every pending tile's polls issued together, then each one
+    // resolved and stored (one round trip for all of them, not one each:
+    // the last waves' drain ends the kernel)
 #pragma unroll
     for (int i = 0; i < D; ++i)
         if (pend[i].valid)
-        {
             pend[i].lb.poll(c);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+        if (pend[i].valid)
             flush_at(i, ~0u);
-        }
 }
 
 }  // namespace qhuff
