@@ -441,23 +441,20 @@ size_string(uint32_t mode, const Src &src, uint32_t rs, uint32_t re,
 // ---- byte-parallel dense pass ------------------------------------------------
 
 // OR the right-aligned len-bit value v (len <= 32; v = 0 when len = 0) into
-// the dense stream at bit pos (words hold their bits MSB first, unswapped);
-// positions past the stream are dropped (the tile then falls back)
+// the dense stream at bit pos (words hold their bits MSB first, unswapped)
 __device__ __forceinline__ void
 dense_or(QH_LDS uint32_t *dense, uint32_t pos, uint32_t v, uint32_t len)
 {
     const uint32_t l = v << ((32u - len) & 31);
     const uint64_t x = ((uint64_t) l << 32) >> (pos & 31);
-    const uint32_t w = pos >> 5;
+    // past the stream: both ORs land on its last two words (the tile then
+    // falls back; no lane branches -- each one cost exec-mask traffic)
+    const uint32_t w = min(pos >> 5, (uint32_t) kDenseWords - 2);
     const uint32_t hi = (uint32_t) (x >> 32), lo = (uint32_t) x;
-    if (w + 1 < (uint32_t) kDenseWords)
-    {
-        __hip_atomic_fetch_or(&dense[w], hi, __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (lo)
-            __hip_atomic_fetch_or(&dense[w + 1], lo, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    __hip_atomic_fetch_or(&dense[w], hi, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(&dense[w + 1], lo, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Byte-parallel pass over the tile's staged chunks (lane l holds span chunks
