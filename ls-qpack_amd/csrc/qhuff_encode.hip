@@ -47,6 +47,8 @@ constexpr int kEncOutCap = kStageCap;         // output stage bytes per tile
 constexpr int kDenseWords = kStageCap / 4 + 4;  // dense code stream (words)
 constexpr uint32_t kDenseBits = 32u * (kDenseWords - 2);
 constexpr int kSpanChunks = kStageCap / 16;   // 16-byte chunks per staged span
+static_assert(64 * kChunks <= kSpanChunks && 16 * kSpanChunks <= kEncOutCap,
+              "dense pass: every row's lens / s0 store in bounds");
 
 struct EncWave                                // one wave's private LDS region
 {
@@ -502,11 +504,9 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
         const uint32_t incl = wave_incl_scan(T);
         const uint32_t p0 = carry + incl - T;
         carry += read_lane(incl, 63);
-        if (c < n16)
-        {
-            lens4[c] = (u32x4){lp[0], lp[1], lp[2], lp[3]};
-            wv->s0[c] = p0;
-        }
+        // c < kSpanChunks always: rows past the span store too (never read)
+        lens4[c] = (u32x4){lp[0], lp[1], lp[2], lp[3]};
+        wv->s0[c] = p0;
         uint32_t pos = p0;
 #pragma unroll
         for (int g = 0; g < 4; ++g)
