@@ -38,7 +38,7 @@ extern "C" {
 
 /* 2: qhuff_huff_decode_ex (the reference's full argument list) added beside
  * the 5-argument qhuff_huff_decode of version 1, which is unchanged */
-#define QHUFF_ABI_VERSION 2
+#define QHUFF_ABI_VERSION 3
 
 /* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
 int qhuff_abi_version(void);
@@ -117,6 +117,49 @@ int qhuff_encode_batch_host(qhuff_ctx *ctx, const uint8_t *in,
 int qhuff_decode_batch_host(qhuff_ctx *ctx, const uint8_t *in,
                             const uint32_t *in_off, uint32_t n, uint8_t *out,
                             uint32_t *out_off, uint8_t *status);
+
+/* ---- low-latency service ----------------------------------------------
+ * The reference codes one literal per call, a few dozen per header block
+ * (lsqpack.c:3718, 3795, 4714, 4824, 4908 decode; 1983-2119 encode).  A
+ * batch call pays a kernel launch, copies and a stream synchronisation; the
+ * service instead keeps a kernel resident on the context's GPU (its own
+ * stream; one workgroup = one CU per 12 request slots) that polls request
+ * slots in pinned host memory: a call writes its strings into a free slot,
+ * the kernel codes them and writes the result back into the slot.
+ *
+ * qhuff_svc_open: attach a service to ctx (one per context) with at least
+ * `slots` request slots (0: 12; at most a quarter of the CUs' worth); its
+ * kernel leaves after idle_us microseconds without a request (0: 20000) and
+ * the next call starts it again.  Once attached, the context's host-path
+ * calls (qhuff_*_batch_host and the per-string entry points below) that fit
+ * a slot go through the service too.
+ *
+ * qhuff_svc_encode / qhuff_svc_decode: the arguments, outputs and return
+ * codes of qhuff_encode_batch_host / qhuff_decode_batch_host; callable from
+ * any number of threads at once (each call takes a free slot, waiting if
+ * none is free).  A call of more than QHUFF_SVC_MAX_STRINGS strings or
+ * QHUFF_SVC_MAX_BYTES input bytes runs the context's host path instead (one
+ * such call at a time).  Offsets must not decrease (QHUFF_EINVAL).
+ *
+ * qhuff_svc_close: stop the kernel and free the service (no call may be in
+ * flight); qhuff_close closes an attached service.  qhuff_svc_stats: calls
+ * served by the kernel, kernel launches, calls sent to the host path. */
+#define QHUFF_SVC_MAX_STRINGS 1024
+#define QHUFF_SVC_MAX_BYTES   65536
+
+typedef struct qhuff_svc qhuff_svc;
+
+int qhuff_svc_open(qhuff_ctx *ctx, unsigned slots, unsigned idle_us,
+                   qhuff_svc **svc_out);
+void qhuff_svc_close(qhuff_svc *svc);
+int qhuff_svc_encode(qhuff_svc *svc, const uint8_t *in, const uint32_t *in_off,
+                     uint32_t n, unsigned mode, uint8_t *out,
+                     uint32_t *out_off);
+int qhuff_svc_decode(qhuff_svc *svc, const uint8_t *in, const uint32_t *in_off,
+                     uint32_t n, uint8_t *out, uint32_t *out_off,
+                     uint8_t *status);
+int qhuff_svc_stats(qhuff_svc *svc, uint64_t *served, uint64_t *launches,
+                    uint64_t *fallbacks);
 
 /* ---- per-string mirrors of the reference entry points -----------------
  * Same argument meaning, return values and error behaviour as the reference

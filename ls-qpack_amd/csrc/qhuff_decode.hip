@@ -23,611 +23,11 @@
 // After the wave scan of the output sizes the arena slots are compacted
 // into the (now dead) input stage and copied out with 16-byte stores once
 // the look-back has resolved the tile's output base.
-#include "qhuff_pipeline.h"
-
-#ifndef QH_DEPTH
-#define QH_DEPTH 3
-#endif
-// bytes past the last slot's bound (the two-byte emitter writes one past
-// its end)
-#ifndef QH_ARENA_SLACK
-#define QH_ARENA_SLACK 16
-#endif
+#include "qhuff_decode_impl.h"
 
 namespace qhuff {
 
-
-// window entry fields (qhuff_tables.h)
-__device__ __forceinline__ uint32_t ent_c(uint32_t e) { return (e >> 8) & 15; }
-__device__ __forceinline__ uint32_t ent_l0(uint32_t e) { return (e >> 12) & 15; }
-__device__ __forceinline__ uint32_t ent_ns(uint32_t e) { return (e >> 24) & 3; }
-__device__ __forceinline__ uint32_t ent_sym1(uint32_t e) { return (e >> 16) & 0xff; }
-
-// staged input bytes (the output stage, the dead input stage, always has the
-// chunk registers' 3,072); a smaller cap lets more waves fit the LDS (16
-// waves at 2,816 B were slower: dec 88 vs 86 us, round 1)
-constexpr int kDecNch = kChunks;                        // chunks per lane
-constexpr uint32_t kDecTS = kWT;                        // strings per tile
-constexpr int kDecStageCap = 64 * kDecNch * 16;
-#ifndef QH_DEC_IN_CAP
-#define QH_DEC_IN_CAP 3072
-#endif
-constexpr int kDecInCap = QH_DEC_IN_CAP;
-static_assert(kDecInCap % 16 == 0 && kDecInCap <= kDecStageCap, "input cap");
-// byte slot of string i: 2i + floor(8 * (rs_i - A) / 5) -- an output is at
-// most 8/5 of its input, plus one byte written past the end by the
-// two-byte emitter
-constexpr int kVarArenaBytes = 2 * kDecTS + 8 * kDecInCap / 5 + QH_ARENA_SLACK;
-// Tiles whose strings are all short enough use a fixed-stride arena
-// instead: lane l's slot at kFixStride * l.  The stride is an odd number of
-// dwords, so the byte stores of lanes that have emitted about as many
-// bytes fall on distinct banks (with slots placed by input offset the 64
-// stores of a step land on random banks: the stores were two thirds of the
-// step loop's LDS bank-conflict cycles, profiles/r03_b).  A string of at
-// most kFixMaxLen Huffman bytes decodes to at most floor(8 * len / 5) bytes
-// and the emitter writes one past its end.
-#ifndef QH_FIX_STRIDE
-#define QH_FIX_STRIDE 108
-#endif
-constexpr uint32_t kFixStride = QH_FIX_STRIDE;
-static_assert(kFixStride % 8 == 4, "an odd number of dwords");
-constexpr uint32_t kFixMaxLen = (5 * (kFixStride - 1)) / 8;
-constexpr int kArenaBytes = kVarArenaBytes > (int) (64 * kFixStride)
-                          ? kVarArenaBytes : (int) (64 * kFixStride);
-
-struct DecWave                       // one wave's private LDS region
-{
-    alignas(16) uint32_t in[kDecStageCap / 4];   // BE input dwords; output stage
-    alignas(16) uint8_t arena[kArenaBytes];
-};
-
-// hold entry, one past the window table: c = 0, ns = 0, not a long code
-constexpr uint32_t kHoldIdx = kWinSize;
-constexpr uint32_t kHoldEntry = 1u << 26;
-
-struct DecSmem
-{
-    uint32_t win[kWinSize + 4];      // + the hold entry
-    uint16_t sorted[257];
-    DecWave w[kWaves];
-    BlockTickets tk;                 // the workgroup's first tickets
-};
-
-struct DecLds                        // big-endian dwords staged in LDS
-{
-    const QH_LDS uint32_t *w;
-    __device__ __forceinline__ uint32_t dw(uint32_t i) const { return w[i]; }
-    // the stage has slack past the input: reading ahead is always safe
-    __device__ __forceinline__ uint32_t dw_ahead(uint32_t i, uint32_t) const
-    {
-        return w[i];
-    }
-};
-struct DecGlb                        // raw little-endian bytes in global
-{
-    const QH_GLB uint32_t *w;
-    __device__ __forceinline__ uint32_t dw(uint32_t i) const
-    {
-        return bswap32(w[i]);
-    }
-    // never touch a dword that holds no byte of the string (page safety)
-    __device__ __forceinline__ uint32_t dw_ahead(uint32_t i,
-                                                 uint32_t bitend) const
-    {
-        return i * 32 < bitend ? bswap32(w[i]) : 0u;
-    }
-};
-
-// long-code step: canonical search over the code lengths 13..30 (compile-
-// time parameters, one compare-and-select per length)
-template <int I>
-__device__ __forceinline__ void
-long_search(uint32_t w, uint32_t &L, uint32_t &idx)
-{
-    if constexpr (I < (int) kLongTab.n)
-    {
-        constexpr LongLen ll = kLongTab.l[I];
-        const uint32_t off = (w >> (32 - ll.len)) - ll.first;
-        const bool hit = (L == 0) & (off < ll.count);
-        L = hit ? ll.len : L;
-        idx = hit ? ll.base + off : idx;
-        long_search<I + 1>(w, L, idx);
-    }
-}
-
-__device__ __forceinline__ uint32_t
-long_code(uint32_t w, const QH_LDS uint16_t *s_sorted, uint32_t *len)
-{
-    uint32_t L = 0, idx = 0;
-    long_search<0>(w, L, idx);
-    *len = L;
-    return s_sorted[idx];
-}
-
-// One main-phase step: look the top 12 bits up, emit up to two symbols,
-// shift them out of the 64-bit buffer hi:lo and refill one dword when fewer
-// than 32 valid bits remain.  GATED: lanes with act == false keep their
-// state (consume 0 bits, emit 0 bytes).  Returns false for a lane that hit
-// the EOS code (the string is rejected, D3 (a)).
-template <bool GATED, class Emit>
-__device__ __forceinline__ bool
-main_step(bool act, uint32_t d, uint32_t &hi, uint32_t &lo, uint32_t &bits,
-          uint32_t &rem, uint32_t &p, const QH_LDS uint32_t *s_win,
-          const QH_LDS uint16_t *s_sorted, Emit &emit)
-{
-    uint32_t e = s_win[hi >> (32 - kWinBits)];
-    bool ok = true;
-    if (__builtin_amdgcn_ballot_w64((GATED ? act : true) & (e < (1u << 24))))
-    {
-        // a code of 13..30 bits: synthesize the entry of a one-symbol step
-        uint32_t L;
-        const uint32_t sym = long_code(hi, s_sorted, &L);
-        const bool lng = (GATED ? act : true) & (e < (1u << 24));
-        ok = !(lng & (sym == 256));
-        const uint32_t el = (sym & 0xff) | (L << 8) | (L << 12) | (1u << 24)
-                          | ((32u - L) << 26);
-        e = lng ? (ok ? el : 0u) : e;
-    }
-    if (GATED)
-        e = act ? e : 0u;
-    const uint32_t nb = (e >> 24) & 3;       // 0 for a held lane
-    const uint32_t k = e >> 26;              // 32 - bits consumed
-    const uint32_t cc = 32u - k;
-    emit(e, nb);
-    const uint32_t sh = __builtin_amdgcn_alignbit(hi, lo, k);
-    hi = GATED ? (nb ? sh : hi) : sh;
-    lo = lo << (cc & 31);                    // held: cc = 32, no shift
-    const uint32_t used = GATED ? (nb ? cc : 0u) : cc;
-    bits -= used;
-    rem -= used;
-    const bool need = bits < 32;
-    const uint32_t dd = need ? d : 0u;
-    hi |= dd >> (bits & 31);
-    lo |= dd << ((32 - bits) & 31);
-    p += need ? 1 : 0;
-    bits += need ? 32 : 0;
-    return ok;
-}
-
-// Decode one string whose bits are [bit0, bitend) of the big-endian dword
-// stream `src`; emitted bytes go through `emit`.  Returns the number of
-// output bytes, or -1 for a rejected string.  Three wave-uniform phases:
-//   1. while every lane has >= 32 real bits ahead: ungated steps;
-//   2. while some lane does: steps predicated on the lane's own state;
-//   3. the last < 32 bits, padded with ones, with the D3 tail rule.
-template <class Src, class Emit>
-__device__ __forceinline__ int
-decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
-              const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
-              Emit &emit)
-{
-    uint32_t rem = bitend - bit0;            // real bits not yet consumed
-    uint32_t hi = 0, lo = 0, bits = 0, p = 0;
-    if (rem)
-    {
-        const uint32_t i0 = bit0 >> 5, sk = bit0 & 31;
-        const uint32_t a = src.dw(i0), b = src.dw_ahead(i0 + 1, bitend);
-        hi = sk ? __builtin_amdgcn_alignbit(a, b, 32 - sk) : a;
-        lo = b << sk;
-        bits = 64 - sk;
-        p = i0 + 2;
-    }
-    bool bad = false;
-
-    // Invariant in phases 1-2: the buffer holds >= 32 valid bits and ends
-    // on a dword boundary (p).  A held lane's two arena byte writes land at
-    // its current end and are overwritten or ignored.
-    if (!__builtin_amdgcn_ballot_w64(rem < 32))
-    do
-    {
-        const uint32_t d = src.dw_ahead(p, bitend);
-        const bool ok = main_step<false>(true, d, hi, lo, bits, rem, p, s_win,
-                                         s_sorted, emit);
-        bad |= !ok;
-        rem = ok ? rem : 0u;                 // leave phase 1 (rare)
-    } while (!__builtin_amdgcn_ballot_w64(rem < 32));
-    bool act = rem >= 32 && !bad;
-    if (__builtin_amdgcn_ballot_w64(act))
-    do
-    {
-        const uint32_t d = src.dw_ahead(p, bitend);
-        const bool ok = main_step<true>(act, d, hi, lo, bits, rem, p, s_win,
-                                        s_sorted, emit);
-        bad |= !ok;
-        act = act & ok & (rem >= 32);
-    } while (__builtin_amdgcn_ballot_w64(act));
-
-    // epilogue: the last < 32 bits, padded with ones; D3 tail rule
-    bool fin = bad || rem == 0;
-    if (__builtin_amdgcn_ballot_w64(!fin))
-    do
-    {
-        const uint32_t w = hi | (0xffffffffu >> (rem & 31));
-        const uint32_t e = s_win[w >> (32 - kWinBits)];
-        const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
-        const bool two = (ns == 2) & (ct <= rem);
-        uint32_t c = two ? ct : (ns ? l0 : 31u);
-        uint32_t val = e;
-        bool eos = false;
-        if (__builtin_amdgcn_ballot_w64(!fin & (ns == 0) & (rem > kWinBits)))
-        {
-            uint32_t L;
-            const uint32_t sym = long_code(w, s_sorted, &L);
-            const bool lng = (ns == 0) & (rem > kWinBits);
-            c = lng ? L : c;
-            val = lng ? sym : val;
-            eos = lng & (sym == 256);
-        }
-        // c > rem: what is left is padding -- at most 7 bits of EOS prefix
-        const bool over = c > rem;
-        const uint32_t ones = 0xffffffffu >> ((32 - rem) & 31);
-        const bool tail_bad = rem >= 8 || (w >> ((32 - rem) & 31)) != ones;
-        const bool live = !fin;
-        bad |= live & ((over & tail_bad) | (!over & eos));
-        const bool step = live & !over & !eos;
-        const uint32_t nb = step ? (two ? 2u : 1u) : 0u;
-        c = step ? c : 0;
-        emit(val, nb);
-        const uint32_t sh = __builtin_amdgcn_alignbit(hi, lo, (32 - c) & 31);
-        hi = c ? sh : hi;
-        lo = lo << (c & 31);
-        rem -= c;
-        fin = fin | over | eos | (rem == 0);
-    } while (__builtin_amdgcn_ballot_w64(!fin));
-    return bad ? -1 : (int) emit.n;
-}
-
-// Lean variant used by the staged (LDS) path.  The bit stream sits in two
-// dwords A:B with a position t: the 32-bit window is alignbit(A, B, t) --
-// ((A:B) >> t), the next bit at A's bit 31 - (32 - t) -- valid for t in
-// [0, 31] (t = 0: the window is B).  Consuming c bits lowers t; when it goes
-// negative the window moves on a dword (A = B, B = the next dword, read one
-// step ahead) and t wraps (t & 31).  No 64-bit shifts, and the window always
-// holds 32 stream bits, enough for any code.  Main steps run while a lane
-// has at least kWinBits real bits left, so the window's top kWinBits bits
-// hold no padding and every symbol of its entry is real (a lane past that
-// reads the hold entry: it consumes and emits nothing); the EOS check and
-// the "code runs past the end" check (the leftover would be >= 8 bits: D3)
-// live in the rare long-code branch.  The last < kWinBits bits (at most two
-// symbols) take the padded epilogue with the D3 tail rule, exactly as
-// decode_string().
-template <class Emit>
-__device__ __forceinline__ int
-decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
-                  const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
-                  Emit &emit)
-{
-    uint32_t rem = bitend - bit0;            // real bits not yet consumed
-    uint32_t A, B, t, p, nx;
-    {
-        const uint32_t i0 = bit0 >> 5, sk = bit0 & 31;
-        A = src[i0];
-        const uint32_t a1 = src[i0 + 1];
-        B = sk ? a1 : A;                     // sk == 0: the window is B = A
-        t = (32 - sk) & 31;
-        p = sk ? i0 + 2 : i0 + 1;
-        nx = src[p];
-    }
-    uint32_t bad = 0;                        // (a u32: no lane-mask phis)
-    // No lane branches in the step: a lane with < kWinBits real bits left
-    // looks up the hold entry (c = ns = 0, never a long code); its two arena
-    // byte writes land at its current end and are overwritten by the
-    // epilogue.
-    constexpr uint32_t kMain = kWinBits;
-    uint32_t W = __builtin_amdgcn_alignbit(A, B, t);
-    // idx is the entry's byte offset: (W >> 17) & 0x7ffc for a live lane,
-    // the hold entry's for a held one -- one v_and_or on the step's chain
-    // (the two masks come off the rem compare, beside it).  (One select
-    // after the masked shift, a VALU fewer but one longer on the chain, was
-    // neutral: dec 66.16 vs 66.21 us, profiles/r02_r/ab_addr2.txt.)
-    auto win_addr = [](uint32_t w, bool live) -> uint32_t {
-        return ((w >> (32 - kWinBits - 2)) & (live ? 4u * (kWinSize - 1) : 0u))
-             | (live ? 0u : 4u * kHoldIdx);
-    };
-    uint32_t idx = win_addr(W, rem >= kMain);
-    // A long-code marker entry (e < 2^24: c = ns = 0) stalls its lane where
-    // it is, like the hold entry.  The step loop runs while some lane with
-    // >= kMain bits left is not stalled -- so the step carries no long-code
-    // branch -- and the stalled lanes then take their long step together,
-    // outside the loop, and the loop resumes.
-    auto advance = [&](uint32_t c) {
-        uint32_t tn;
-        const bool cross = __builtin_sub_overflow(t, c, &tn);
-        A = cross ? B : A;
-        B = cross ? nx : B;
-        t = tn & 31;
-        p += cross ? 1u : 0u;
-    };
-    for (;;)
-    {
-        uint32_t e = kHoldEntry;
-        if (__builtin_amdgcn_ballot_w64(rem >= kMain))
-        do
-        {
-            e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
-            const uint32_t c = ent_c(e);
-            emit(e, ent_ns(e));
-            rem -= c;
-            advance(c);
-            nx = src[p];
-            W = __builtin_amdgcn_alignbit(A, B, t);
-            idx = win_addr(W, rem >= kMain);
-        } while (__builtin_amdgcn_ballot_w64((rem >= kMain) & (e >= (1u << 24))));
-        // lanes left with >= kMain bits sit on a code of 14..30 bits; EOS,
-        // or a code running past the end, rejects the string (D3)
-        if (__builtin_expect(!__builtin_amdgcn_ballot_w64(rem >= kMain), 1))
-            break;
-        const bool lng = rem >= kMain;
-        uint32_t L;
-        const uint32_t sym = long_code(W, s_sorted, &L);
-        const bool rej = lng & ((sym == 256) | (L > rem));
-        const bool ok = lng & !rej;
-        const uint32_t c = ok ? L : 0u;
-        emit(sym, ok ? 1u : 0u);
-        bad |= rej ? 1u : 0u;
-        rem = rej ? 0u : rem - c;
-        advance(c);
-        nx = src[p];
-        W = __builtin_amdgcn_alignbit(A, B, t);
-        idx = win_addr(W, rem >= kMain);
-    }
-
-    // epilogue, one pass: the last < kWinBits (13) real bits hold at most
-    // two symbols (codes are >= 5 bits), both inside the window padded with
-    // ones, so one lookup decodes them; the bits after them cannot complete
-    // a code (its entry would have decoded it), so they are the padding, and
-    // the D3 tail rule (fewer than 8 bits, all ones) applies at once.  The
-    // EOS code (30 bits) cannot occur in 12 bits.
-    {
-        const bool live = !(bad || rem == 0);
-        const uint32_t w = W | (0xffffffffu >> (rem & 31));
-        const uint32_t e = s_win[w >> (32 - kWinBits)];
-        const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
-        const bool two = (ns == 2) & (ct <= rem);
-        const bool one = !two & (ns != 0) & (l0 <= rem);
-        const uint32_t c = two ? ct : (one ? l0 : 0u);
-        emit(e, live ? (two ? 2u : (one ? 1u : 0u)) : 0u);
-        const uint32_t r2 = rem - c;             // padding bits
-        const uint32_t inv = ~(w << (c & 31));   // padding bits at the top
-        const bool pad_ok = r2 < 8 && (r2 == 0 || (inv >> ((32 - r2) & 31)) == 0);
-        bad |= (live & !pad_ok) ? 1u : 0u;
-    }
-    emit.finish();
-    return bad ? -1 : (int) emit.n;
-}
-
-// byte-granular arena sink: two unconditional byte stores per step, the
-// entry's first symbol [7:0] and second [23:16] (ds_write_b8 / _d16_hi; the
-// second is overwritten by the next step when only one symbol was emitted)
-struct ArenaEmit
-{
-    QH_LDS uint8_t *slot;
-    QH_LDS uint8_t *p;
-    uint32_t n;
-    __device__ __forceinline__ void finish() { n = (uint32_t) (p - slot); }
-    __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
-    {
-        // (exec-masked for held lanes only: slower, profiles/r02_e)
-        p[0] = (uint8_t) val;
-        p[1] = (uint8_t) (val >> 16);
-        p += nb;
-    }
-};
-
-struct CountEmit
-{
-    uint32_t n;
-    __device__ __forceinline__ void operator()(uint32_t, uint32_t nb)
-    {
-        n += nb;
-    }
-};
-
-struct GlobalEmit                            // slow path: byte stores
-{
-    uint8_t *dst;
-    uint32_t n;
-    __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
-    {
-        if (nb >= 1)
-            dst[n] = (uint8_t) val;
-        if (nb == 2)
-            dst[n + 1] = (uint8_t) (val >> 16);
-        n += nb;
-    }
-};
-
-// arena slot -> stage at byte D (wave-synchronous; other lanes write the
-// neighbouring bytes).  Bytes up to D's dword boundary (head) and after the
-// last whole dword (tail) by byte stores, the whole dwords between from pairs
-// of aligned source words (alignbyte), four per trip with the reads of a trip
-// issued together: per trip one LDS round trip, not one per dword.
-__device__ __forceinline__ void
-write_bytes(QH_LDS uint8_t *d, uint32_t v, uint32_t nb)
-{
-    if (nb > 0)
-        d[0] = (uint8_t) v;
-    if (nb > 1)
-        d[1] = (uint8_t) (v >> 8);
-    if (nb > 2)
-        d[2] = (uint8_t) (v >> 16);
-}
-
-__device__ __forceinline__ void
-compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
-{
-    uint32_t h = (4 - ((uint32_t) (uintptr_t) dstb & 3)) & 3;
-    h = h < n ? h : n;
-    const uint32_t nb = (n - h) >> 2;
-    const uint32_t nt = n - h - 4 * nb;
-    const uint32_t sa = (uint32_t) (uintptr_t) src;
-    const QH_LDS uint32_t *sw = (const QH_LDS uint32_t *) (src - (sa & 3));
-    const uint32_t s3 = sa & 3;
-    // head and tail: the 4 source bytes at src + i, i = 0 and h + 4 nb
-    const uint32_t it = h + 4 * nb;
-    const uint32_t qt = (s3 + it) >> 2;
-    const uint32_t vh = h ? align_bytes(sw[1], sw[0], s3) : 0u;
-    const uint32_t vt = nt ? align_bytes(sw[qt + 1], sw[qt], (s3 + it) & 3) : 0u;
-    // body: source words from q0, shift r
-    const uint32_t sb = s3 + h, r = sb & 3;
-    const QH_LDS uint32_t *bw = sw + (sb >> 2);
-    QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
-    // Eight dwords per trip, the trip's source words read together and the
-    // last one carried into the next trip (reads past the string stay in
-    // the wave's LDS region or past the allocation, where LDS reads 0).
-    // The first trip's reads go out with the head's and tail's, before any
-    // write (the arena and the stage do not overlap; a wave's LDS operations
-    // run in order, so a read behind a write would wait for it).
-    uint32_t cur = bw[0];
-    uint32_t nw[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        nw[j] = bw[j + 1];
-    write_bytes(dstb, vh, h);
-    write_bytes(dstb + it, vt, nt);
-    for (uint32_t k = 0; k < nb; k += 8)
-    {
-        if (k)
-        {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                nw[j] = bw[k + j + 1];
-        }
-        dw[k] = align_bytes(nw[0], cur, r);
-#pragma unroll
-        for (int j = 1; j < 8; ++j)
-            if (k + j < nb)
-                dw[k + j] = align_bytes(nw[j], nw[j - 1], r);
-        cur = nw[7];
-    }
-}
-
-// A tile whose input or output does not fit the stage, coded eagerly:
-// input staged -> the arena already holds the bytes (sz / st given);
-// otherwise count from global memory, then decode again to global.  Out of
-// line (cold), state by value.
-__device__ __noinline__ void
-dec_slow_tile(const uint8_t *in, QH_LDS DecSmem *sm, QH_LDS DecWave *wv,
-              uint32_t slot0, Coord c, uint32_t t, uint32_t cnt, TileOffs to,
-              Span sp, uint32_t sz, uint32_t st, uint8_t *out,
-              uint32_t *out_off, uint8_t *status, uint64_t n)
-{
-    const uint32_t lane = lane_id();
-    const bool valid = lane < cnt;
-    const uint32_t rs = valid ? (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa) : 0;
-    const uint32_t re = valid ? (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa) : 0;
-    const DecGlb src{(const QH_GLB uint32_t *) sp.pa};
-    if (!sp.staged)
-    {
-        int r = 0;
-        if (valid)
-        {
-            CountEmit em{0};
-            r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted, em);
-        }
-        sz = r < 0 ? 0u : (uint32_t) r;
-        st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
-    }
-    const uint32_t incl = wave_incl_scan(sz);
-    const uint32_t excl = incl - sz;
-    const uint32_t total = read_lane(incl, 63);
-    LookBack lb;
-    lb.start(c, t, total);
-    lb.super_agg(c);
-    lb.poll(c);
-    const uint64_t base = lb.finish(c);
-    uint8_t *dst = out + base + excl;
-    if (sp.staged)
-    {
-        const QH_LDS uint8_t *sa = wv->arena + slot0;
-        for (uint32_t i = 0; i < sz; ++i)
-            ((QH_GLB uint8_t *) dst)[i] = sa[i];
-    }
-    else if (valid && st == QHUFF_DEC_OK && sz)
-    {
-        GlobalEmit em{dst, 0};
-        decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted, em);
-    }
-    const uint64_t s0 = (uint64_t) t * kWT;
-    if (valid)
-    {
-        ((QH_GLB uint32_t *) out_off)[s0 + lane] = (uint32_t) (base + excl);
-        ((QH_GLB uint8_t *) status)[s0 + lane] = (uint8_t) st;
-    }
-    if (t == c.n_tiles - 1 && lane == 0)
-    {
-        ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) (base + total);
-        if (base + total > 0xffffffffull)        // offsets are 32-bit
-            raise_error(c, kErrRange);
-    }
-}
-
-// the decode side of the wave pipeline (qhuff_pipeline.h)
-struct DecPolicy
-{
-    static constexpr bool kStatus = true;
-    static constexpr int kInCap = kDecInCap;
-    static constexpr int kDepth = QH_DEPTH;       // pending tiles
-    static constexpr int kOutCap = kDecStageCap;
-    static constexpr int kNch = kDecNch;          // 16-byte chunks per lane
-    static constexpr uint32_t kTS = kDecTS;       // strings per tile
-    using Offs = TileOffs;
-    const uint8_t *in;
-    QH_LDS DecSmem *sm;
-    QH_LDS DecWave *wv;
-    uint32_t slot0;                  // this lane's arena slot (current tile)
-
-    __device__ __forceinline__ void stage_in(const Chunks<kNch> &ch,
-                                             const Span &sp, const Offs &)
-    {
-        ch.store<true>((QH_LDS u32x4 *) wv->in, sp.n16);
-    }
-    __device__ __forceinline__ void prepare(const Span &) {}
-    __device__ __forceinline__ const QH_LDS uint32_t *out_stage() const
-    {
-        return wv->in;
-    }
-    // staged tile: decode this lane's string into its arena slot
-    __device__ __forceinline__ void codec(const Offs &to, uint32_t cnt,
-                                          const Span &sp, uint32_t *sz,
-                                          uint32_t *st)
-    {
-        const uint32_t lane = lane_id();
-        const uint32_t A = to.first();
-        const bool fixed = !__builtin_amdgcn_ballot_w64(
-            (lane < cnt) & (to.o1 - to.o0 > kFixMaxLen));
-        slot0 = fixed ? kFixStride * lane
-                      : 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
-        int r = 0;
-        if (lane < cnt)
-        {
-            const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
-            const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
-            ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
-            r = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted,
-                                  em);
-        }
-        *sz = r < 0 ? 0u : (uint32_t) r;
-        *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
-    }
-    // arena -> the (dead) input stage, compacted
-    __device__ __forceinline__ void emit(uint32_t excl, uint32_t sz, uint32_t)
-    {
-        if (sz)
-            compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
-                           sz);
-    }
-
-    __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
-                                              Offs to, Span sp, uint32_t sz,
-                                              uint32_t st, uint8_t *out,
-                                              uint32_t *out_off, uint8_t *status,
-                                              uint64_t n)
-    {
-        dec_slow_tile(in, sm, wv, slot0, c, t, cnt, to, sp, sz, st, out,
-                      out_off, status, n);
-    }
-};
+using DecPolicy = DecPolicyT<DecSmem>;
 
 __global__ __launch_bounds__(64 * kWaves) void
 qhuff_decode_kernel(DecArgs a)

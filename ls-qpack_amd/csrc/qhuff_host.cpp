@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -175,6 +176,9 @@ struct qhuff_ctx
     // error an earlier (completed) launch left without synchronising
     uint32_t *err_host;
     uint32_t *err_host_dev;
+    // the low-latency service attached by qhuff_svc_open (small host-path
+    // calls on this context go through it)
+    qhuff_svc *svc;
     char err_msg[256];
 };
 
@@ -319,6 +323,8 @@ qhuff_close(qhuff_ctx *c)
     if (!c)
         return;
     (void) hipSetDevice(c->device);
+    if (c->svc)
+        qhuff_svc_close(c->svc);
     if (c->own_stream)
         (void) hipStreamSynchronize(c->own_stream);
     (void) hipDeviceSynchronize();
@@ -860,6 +866,11 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
     return QHUFF_OK;
 }
 
+static bool svc_fits(const uint32_t *in_off, uint32_t n);
+static int svc_call(qhuff_svc *v, bool enc, const uint8_t *in,
+                    const uint32_t *in_off, uint32_t n, unsigned mode,
+                    uint8_t *out, uint32_t *out_off, uint8_t *status);
+
 extern "C" int
 qhuff_encode_batch_host(qhuff_ctx *c, const uint8_t *in,
                         const uint32_t *in_off, uint32_t n, unsigned mode,
@@ -867,6 +878,8 @@ qhuff_encode_batch_host(qhuff_ctx *c, const uint8_t *in,
 {
     if (mode != 0 && mode != 3 && mode != 5 && mode != 7)
         return QHUFF_EINVAL;
+    if (c && c->svc && in_off && svc_fits(in_off, n))
+        return svc_call(c->svc, true, in, in_off, n, mode, out, out_off, nullptr);
     return host_batch(c, true, in, in_off, n, mode, out, out_off, nullptr);
 }
 
@@ -875,7 +888,383 @@ qhuff_decode_batch_host(qhuff_ctx *c, const uint8_t *in,
                         const uint32_t *in_off, uint32_t n, uint8_t *out,
                         uint32_t *out_off, uint8_t *status)
 {
+    if (c && c->svc && in_off && svc_fits(in_off, n))
+        return svc_call(c->svc, false, in, in_off, n, 0, out, out_off, status);
     return host_batch(c, false, in, in_off, n, 0, out, out_off, status);
+}
+
+// ---- low-latency service (qhuff_service.hip) -----------------------------------
+//
+// The resident kernel's request slots live in pinned, device-mapped host
+// memory (fine-grained: the device's loads and stores of a slot go over PCIe
+// and are coherent with the host's).  A call takes a free slot, writes the
+// rebased offsets, the bytes and the header, then the request sequence
+// number (release); it spins on the slot's done word (acquire), copies the
+// results out and frees the slot.  The kernel is (re)started on demand: at
+// the first call, and by a waiting call that finds the service stream idle
+// (the waves leave after idle_us without requests).
+
+struct qhuff_svc
+{
+    qhuff_ctx *ctx;
+    hipStream_t stream;              // the resident kernel's own stream
+    uint8_t *slots_h, *slots_d;      // pinned slots, host / device views
+    uint32_t *ctl_h, *ctl_d;         // pinned control word: [0] stop
+    uint8_t *scratch;                // device: kSvcScratchBytes per slot
+    uint64_t *active;                // device: last serve time (100 MHz)
+    uint32_t n_slots, grid;
+    uint64_t idle_ticks, life_ticks;
+    std::atomic<uint32_t> *busy;     // per slot: 0 free, 1 taken
+    uint32_t *seq;                   // per slot: last posted sequence
+    std::atomic<uint32_t> next_slot{0};
+    std::mutex launch_mu;            // (re)launch of the kernel
+    std::mutex fallback_mu;          // large requests: the context's host path
+    std::atomic<uint64_t> served{0}, launches{0}, fallbacks{0};
+};
+
+static inline SvcHdr *
+svc_hdr(qhuff_svc *v, uint32_t k)
+{
+    return (SvcHdr *) (v->slots_h + (size_t) k * kSvcSlotBytes);
+}
+
+static bool
+svc_fits(const uint32_t *in_off, uint32_t n)
+{
+    return n <= kSvcMaxStrings && (uint64_t) in_off[n] - in_off[0] <= kSvcInCap
+           && in_off[n] >= in_off[0];
+}
+
+// start the kernel if its stream is idle (a previous instance has left)
+static int
+svc_ensure_running(qhuff_svc *v)
+{
+    std::lock_guard<std::mutex> g(v->launch_mu);
+    qhuff_ctx *c = v->ctx;
+    const hipError_t q = hipStreamQuery(v->stream);
+    if (q == hipErrorNotReady)
+        return QHUFF_OK;
+    if (q != hipSuccess)
+        return fail(c, q, "hipStreamQuery(service)");
+    HIPCHK(c, hipSetDevice(c->device));
+    __atomic_store_n(&v->ctl_h[0], 0u, __ATOMIC_RELEASE);
+    HIPCHK(c, hipMemsetAsync(v->active, 0, sizeof(uint64_t), v->stream));
+    SvcArgs a;
+    a.slots = v->slots_d;
+    a.scratch = v->scratch;
+    a.ctl = v->ctl_d;
+    a.active = v->active;
+    a.win = c->tab->win;
+    a.sorted = c->tab->sorted;
+    a.enc = c->tab->enc;
+    a.idle_ticks = v->idle_ticks;
+    a.life_ticks = v->life_ticks;
+    HIPCHK(c, launch_service(a, v->grid, v->stream));
+    v->launches.fetch_add(1, std::memory_order_relaxed);
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_svc_open(qhuff_ctx *c, unsigned slots, unsigned idle_us, qhuff_svc **out)
+{
+    if (!c || !out)
+        return QHUFF_EINVAL;
+    *out = nullptr;
+    if (c->svc)
+        return QHUFF_EINVAL;                     // one service per context
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint32_t wpb = (uint32_t) service_waves_per_block();
+    uint32_t grid = slots ? (slots + wpb - 1) / wpb : 1;
+    if (grid > (uint32_t) c->n_cu / 4)
+        grid = (uint32_t) c->n_cu / 4;           // at most a quarter of the CUs
+    if (grid < 1)
+        grid = 1;
+    qhuff_svc *v = new (std::nothrow) qhuff_svc();
+    if (!v)
+        return QHUFF_ENOMEM;
+    v->ctx = c;
+    v->grid = grid;
+    v->n_slots = grid * wpb;
+    v->idle_ticks = 100ull * (idle_us ? idle_us : 20000u);   // 100 MHz clock
+    v->life_ticks = 100ull * 1000000ull * 10;                // 10 s
+    v->busy = new std::atomic<uint32_t>[v->n_slots];
+    v->seq = new uint32_t[v->n_slots];
+    for (uint32_t k = 0; k < v->n_slots; ++k)
+    {
+        v->busy[k].store(0);
+        v->seq[k] = 0;
+    }
+    const size_t sb = (size_t) v->n_slots * kSvcSlotBytes;
+    hipError_t e = hipHostMalloc((void **) &v->slots_h, sb,
+                                 hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess)
+    {
+        memset(v->slots_h, 0, sb);
+        e = hipHostGetDevicePointer((void **) &v->slots_d, v->slots_h, 0);
+    }
+    if (e == hipSuccess)
+        e = hipHostMalloc((void **) &v->ctl_h, 64,
+                          hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess)
+    {
+        memset(v->ctl_h, 0, 64);
+        e = hipHostGetDevicePointer((void **) &v->ctl_d, v->ctl_h, 0);
+    }
+    if (e == hipSuccess)
+        e = hipMalloc((void **) &v->scratch, (size_t) v->n_slots * kSvcScratchBytes);
+    if (e == hipSuccess)
+        e = hipMalloc((void **) &v->active, 64);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking);
+    if (e != hipSuccess)
+    {
+        const int rc = fail(c, e, "service setup");
+        c->svc = v;
+        qhuff_svc_close(v);
+        return rc;
+    }
+    c->svc = v;
+    const int rc = svc_ensure_running(v);
+    if (rc)
+    {
+        qhuff_svc_close(v);
+        return rc;
+    }
+    *out = v;
+    return QHUFF_OK;
+}
+
+extern "C" void
+qhuff_svc_close(qhuff_svc *v)
+{
+    if (!v)
+        return;
+    qhuff_ctx *c = v->ctx;
+    (void) hipSetDevice(c->device);
+    if (v->ctl_h)
+        __atomic_store_n(&v->ctl_h[0], 1u, __ATOMIC_RELEASE);
+    if (v->stream)
+    {
+        (void) hipStreamSynchronize(v->stream);
+        (void) hipStreamDestroy(v->stream);
+    }
+    if (v->scratch)
+        (void) hipFree(v->scratch);
+    if (v->active)
+        (void) hipFree(v->active);
+    if (v->slots_h)
+        (void) hipHostFree(v->slots_h);
+    if (v->ctl_h)
+        (void) hipHostFree(v->ctl_h);
+    delete[] v->busy;
+    delete[] v->seq;
+    if (c->svc == v)
+        c->svc = nullptr;
+    delete v;
+}
+
+extern "C" int
+qhuff_svc_stats(qhuff_svc *v, uint64_t *served, uint64_t *launches,
+                uint64_t *fallbacks)
+{
+    if (!v)
+        return QHUFF_EINVAL;
+    if (served)
+        *served = v->served.load();
+    if (launches)
+        *launches = v->launches.load();
+    if (fallbacks)
+        *fallbacks = v->fallbacks.load();
+    return QHUFF_OK;
+}
+
+// take a free slot (spinning / yielding while none is); try_only: return
+// n_slots at once if none is free
+static uint32_t
+svc_take(qhuff_svc *v, bool try_only)
+{
+    uint32_t k = v->next_slot.fetch_add(1, std::memory_order_relaxed) % v->n_slots;
+    for (uint32_t tries = 0;; ++tries)
+    {
+        uint32_t z = 0;
+        if (v->busy[k].compare_exchange_strong(z, 1, std::memory_order_acquire))
+            return k;
+        k = (k + 1) % v->n_slots;
+        if (tries % v->n_slots == v->n_slots - 1)
+        {
+            if (try_only)
+                return v->n_slots;
+            std::this_thread::yield();
+        }
+    }
+}
+
+// write strings [s0, s1) of the call into slot k and post it; returns the
+// request's sequence number
+static uint32_t
+svc_post(qhuff_svc *v, uint32_t k, bool enc, const uint8_t *in,
+         const uint32_t *in_off, uint32_t s0, uint32_t s1, unsigned mode)
+{
+    uint8_t *sb = v->slots_h + (size_t) k * kSvcSlotBytes;
+    SvcHdr *h = svc_hdr(v, k);
+    const uint32_t n = s1 - s0, a0 = in_off[s0], nb = in_off[s1] - a0;
+    uint32_t *so = (uint32_t *) (sb + kSvcInOffAt);
+    for (uint32_t i = 0; i <= n; ++i)
+        so[i] = in_off[s0 + i] - a0;
+    if (nb)
+        memcpy(sb + kSvcInAt, in + a0, nb);
+    h->op = enc ? kSvcOpEncode : kSvcOpDecode;
+    h->n = n;
+    h->mode = mode;
+    h->in_bytes = nb;
+    const uint32_t sq = v->seq[k] + 1 ? v->seq[k] + 1 : 1;
+    v->seq[k] = sq;
+    __atomic_store_n(&h->req, sq, __ATOMIC_RELEASE);
+    return sq;
+}
+
+// Wait for slot k's request sq: spin on the done word; every ~50 us check
+// that the kernel still runs (its waves leave after idle_us with no request
+// served, and one may have left just as this request was posted); give up
+// after 10 s (the slot then stays taken).
+static int
+svc_wait(qhuff_svc *v, uint32_t k, uint32_t sq)
+{
+    SvcHdr *h = svc_hdr(v, k);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto t_chk = t0;
+    for (uint32_t it = 0;; ++it)
+    {
+        if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) == sq)
+            return QHUFF_OK;
+        if ((it & 255) == 255)
+        {
+            const auto now = std::chrono::steady_clock::now();
+            if (now - t_chk > std::chrono::microseconds(50))
+            {
+                t_chk = now;
+                int rc = svc_ensure_running(v);
+                if (rc)
+                    return rc;
+                if (now - t0 > std::chrono::seconds(10))
+                {
+                    snprintf(v->ctx->err_msg, sizeof(v->ctx->err_msg),
+                             "service request timed out");
+                    return QHUFF_EDEVICE;
+                }
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// slot k's result for n strings -> out + base, out_off / status (the
+// piece's first string); returns its output bytes
+static uint32_t
+svc_collect(qhuff_svc *v, uint32_t k, bool enc, uint32_t n, uint32_t base,
+            uint8_t *out, uint32_t *out_off, uint8_t *status)
+{
+    const uint8_t *sb = v->slots_h + (size_t) k * kSvcSlotBytes;
+    const uint32_t *oo = (const uint32_t *) (sb + kSvcOutOffAt);
+    const uint32_t total = oo[n];
+    for (uint32_t i = 0; i < n; ++i)
+        out_off[i] = base + oo[i];
+    if (total)
+        memcpy(out + base, sb + kSvcOutAt, total);
+    if (!enc)
+        memcpy(status, sb + kSvcStatusAt, n);
+    return total;
+}
+
+// A call is cut into pieces of at most one staged tile each (64 strings,
+// kSvcTileBytes input bytes; a longer string alone), one slot per piece: the
+// service codes a one-tile piece straight from its slot, and the pieces of
+// a call run on as many waves at once as there are free slots.
+static int
+svc_call(qhuff_svc *v, bool enc, const uint8_t *in, const uint32_t *in_off,
+         uint32_t n, unsigned mode, uint8_t *out, uint32_t *out_off,
+         uint8_t *status)
+{
+    qhuff_ctx *c = v->ctx;
+    if (!in_off || !out_off || (n && (!in || !out)) || (!enc && n && !status))
+        return QHUFF_EINVAL;
+    if (enc && mode != 0 && mode != 3 && mode != 5 && mode != 7)
+        return QHUFF_EINVAL;
+    if (n == 0)
+    {
+        out_off[0] = 0;
+        return QHUFF_OK;
+    }
+    for (uint32_t i = 0; i < n; ++i)             // the kernel trusts the slot
+        if (in_off[i + 1] < in_off[i])
+            return QHUFF_EINVAL;
+    if (!svc_fits(in_off, n))
+    {
+        // too large for a slot: the context's host path (one caller at a time)
+        std::lock_guard<std::mutex> g(v->fallback_mu);
+        v->fallbacks.fetch_add(1, std::memory_order_relaxed);
+        return host_batch(c, enc, in, in_off, n, mode, out, out_off, status);
+    }
+    constexpr uint32_t kMaxRound = 64;           // pieces in flight per call
+    uint32_t base = 0;
+    uint32_t s0 = 0;
+    while (s0 < n)
+    {
+        // this round's pieces, each in its own slot (the first slot waited
+        // for, further ones only while free)
+        uint32_t slot[kMaxRound], p0[kMaxRound + 1], sq[kMaxRound];
+        uint32_t np = 0;
+        p0[0] = s0;
+        while (s0 < n && np < kMaxRound)
+        {
+            uint32_t s1 = s0 + 1;
+            while (s1 < n && s1 - s0 < (uint32_t) kWT
+                   && in_off[s1 + 1] - in_off[s0] <= kSvcTileBytes)
+                ++s1;
+            const uint32_t k = svc_take(v, np > 0);
+            if (k == v->n_slots)
+                break;
+            slot[np] = k;
+            sq[np] = svc_post(v, k, enc, in, in_off, s0, s1, mode);
+            p0[++np] = s1;
+            s0 = s1;
+        }
+        int rc = svc_ensure_running(v);
+        for (uint32_t j = 0; j < np && !rc; ++j)
+        {
+            rc = svc_wait(v, slot[j], sq[j]);
+            if (!rc)
+            {
+                const uint32_t a = p0[j], m = p0[j + 1] - a;
+                base += svc_collect(v, slot[j], enc, m, base, out, out_off + a,
+                                    enc ? nullptr : status + a);
+                v->busy[slot[j]].store(0, std::memory_order_release);
+            }
+        }
+        if (rc)
+            return rc;                           // (unfinished slots stay taken)
+    }
+    out_off[n] = base;
+    v->served.fetch_add(1, std::memory_order_relaxed);
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_svc_encode(qhuff_svc *v, const uint8_t *in, const uint32_t *in_off,
+                 uint32_t n, unsigned mode, uint8_t *out, uint32_t *out_off)
+{
+    if (!v)
+        return QHUFF_EINVAL;
+    return svc_call(v, true, in, in_off, n, mode, out, out_off, nullptr);
+}
+
+extern "C" int
+qhuff_svc_decode(qhuff_svc *v, const uint8_t *in, const uint32_t *in_off,
+                 uint32_t n, uint8_t *out, uint32_t *out_off, uint8_t *status)
+{
+    if (!v)
+        return QHUFF_EINVAL;
+    return svc_call(v, false, in, in_off, n, 0, out, out_off, status);
 }
 
 // ---- batched literal decode (pre-parsed spans, qhuff_frames.cpp) -----------

@@ -54,6 +54,77 @@ struct HashArgs
     uint32_t pairs;
 };
 
+// ---- low-latency service (qhuff_service.hip, qhuff_svc_* in qhuff_host.cpp)
+//
+// One request slot per service wave, in pinned host memory mapped into the
+// device (fine-grained): the host writes a request and then its sequence
+// number; the wave polls that word, codes the request and writes the result
+// back into the slot, then the done word.  Slot layout (bytes):
+//   header      kSvcHdrBytes   (SvcHdr)
+//   in_off      (n + 1) u32, rebased to 0
+//   in          the request's bytes
+//   out_off     (n + 1) u32
+//   status      n u8 (decode)
+//   out         the output bytes
+constexpr uint32_t kSvcMaxStrings = 1024;     // strings per request
+constexpr uint32_t kSvcInCap = 65536;         // input bytes per request
+constexpr uint32_t kSvcHdrBytes = 256;
+constexpr uint32_t kSvcOffBytes = 4352;       // (kSvcMaxStrings + 1) u32, 256-aligned
+constexpr uint32_t kSvcInOffAt = kSvcHdrBytes;
+constexpr uint32_t kSvcInAt = kSvcInOffAt + kSvcOffBytes;
+constexpr uint32_t kSvcOutOffAt = kSvcInAt + kSvcInCap + 256;
+constexpr uint32_t kSvcStatusAt = kSvcOutOffAt + kSvcOffBytes;
+constexpr uint32_t kSvcOutAt = kSvcStatusAt + kSvcMaxStrings + 256;
+// the encode bound of a full request (qhuff_encode_bound: 30-bit codes, 7
+// bytes of framing per literal, 16 slack), rounded up
+constexpr uint32_t kSvcOutCap =
+    ((kSvcInCap * 30 + 7) / 8 + 7 * kSvcMaxStrings + 16 + 4095) & ~4095u;
+constexpr uint32_t kSvcSlotBytes = (kSvcOutAt + kSvcOutCap + 4095) & ~4095u;
+// device scratch per slot (a request of more than one tile): the slot's
+// layout; in_off and in are copied in, the tile loop reads them and writes
+// out_off, status and out at device-memory latency, and those are copied
+// back into the slot at the end
+constexpr uint32_t kSvcScratchBytes = kSvcSlotBytes;
+static_assert(kSvcInOffAt % 256 == 0 && kSvcInAt % 256 == 0
+              && kSvcOutOffAt % 256 == 0 && kSvcStatusAt % 256 == 0
+              && kSvcOutAt % 256 == 0, "slot regions 256-aligned");
+
+// a piece coded straight from its slot: one staged tile (64 strings, the
+// stage's bytes; qhuff_service.hip checks it against kStageCap)
+constexpr uint32_t kSvcTileBytes = 3072;
+
+constexpr uint32_t kSvcOpDecode = 0;
+constexpr uint32_t kSvcOpEncode = 1;
+
+struct SvcHdr
+{
+    uint32_t req;                // host: sequence of the posted request (last)
+    uint32_t op;                 // kSvcOpDecode / kSvcOpEncode
+    uint32_t n;                  // strings
+    uint32_t mode;               // encode mode
+    uint32_t in_bytes;
+    uint32_t pad0[27];           // (the device's words on their own line)
+    uint32_t done;               // device: sequence of the last served request
+    uint32_t total;              // device: its output bytes
+    uint32_t pad1[30];
+};
+static_assert(sizeof(SvcHdr) <= kSvcHdrBytes, "slot header");
+
+struct SvcArgs
+{
+    uint8_t *slots;              // device view of the pinned slots
+    uint8_t *scratch;            // device memory, kSvcScratchBytes per slot
+    const uint32_t *ctl;         // device view of the pinned control word
+                                 // [0]: stop
+    uint64_t *active;            // device: last time any wave served (100 MHz)
+    const uint32_t *win;
+    const uint16_t *sorted;
+    const uint2 *enc;
+    uint64_t idle_ticks;         // a wave leaves after this long with no
+                                 // request served by any wave (100 MHz ticks)
+    uint64_t life_ticks;         // and after this long in any case
+};
+
 template <class T>
 __device__ __forceinline__ const QH_GLB T *
 glb(const T *p)
@@ -79,5 +150,8 @@ size_t decode_lds_bytes();
 int encode_waves_per_block();
 int decode_waves_per_block();
 uint32_t decode_tile_strings();            // strings per decode tile
+hipError_t launch_service(const SvcArgs &a, uint32_t grid, hipStream_t st);
+int service_waves_per_block();
+size_t service_lds_bytes();
 
 }  // namespace qhuff

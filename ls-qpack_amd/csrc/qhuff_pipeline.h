@@ -54,6 +54,44 @@ struct Pending
     LookBack lb;                     // (its tile and total: lb.tile, lb.total)
 };
 
+// Output base of a slow tile (P::slow_tile / slow_tile_at): the batch
+// kernel's look-back, or a base the caller already has (the service kernel
+// codes a request's tiles in order in one wave).
+struct LookBackBase
+{
+    Coord c;
+    uint32_t t;
+    __device__ __forceinline__ uint64_t operator()(uint32_t total) const
+    {
+        LookBack lb;
+        lb.start(c, t, total);
+        lb.super_agg(c);
+        lb.poll(c);
+        return lb.finish(c);
+    }
+};
+struct FixedBase
+{
+    uint64_t base;
+    __device__ __forceinline__ uint64_t operator()(uint32_t) const
+    {
+        return base;
+    }
+};
+
+// the batch's last tile: the closing offset (and the 32-bit range check)
+__device__ __forceinline__ void
+last_tile_end(const Coord &c, uint32_t t, uint64_t end, uint32_t *out_off,
+              uint64_t n)
+{
+    if (t == c.n_tiles - 1 && lane_id() == 0)
+    {
+        ((QH_GLB uint32_t *) out_off)[n] = (uint32_t) end;
+        if (end > 0xffffffffull)                 // offsets are 32-bit
+            raise_error(c, kErrRange);
+    }
+}
+
 // resolve a pending tile's base and store it from `o` (every lane)
 template <class P>
 __device__ __forceinline__ void

@@ -33,6 +33,8 @@ EXPORTS = (
     "qhuff_scan_field_section", "qhuff_scan_encoder_stream",
     "qhuff_literals_bound", "qhuff_decode_literals_host",
     "qhuff_frame_literal", "qhuff_xxh32_headers_host",
+    "qhuff_svc_open", "qhuff_svc_close", "qhuff_svc_encode",
+    "qhuff_svc_decode", "qhuff_svc_stats",
     # include/qhuff_lsqpack.h
     "qhuff_lsqpack_enc_enc_str", "qhuff_lsqpack_huff_decode",
     "qhuff_lsqpack_set_decode_full", "qhuff_lsqpack_set_device",
@@ -168,6 +170,20 @@ def lib():
         L.qhuff_xxh32_headers_host.restype = C.c_int
         L.qhuff_xxh32_headers_host.argtypes = [vp, vp, u32p, C.c_uint32,
                                                C.c_uint32, u32p, u32p]
+        L.qhuff_svc_open.restype = C.c_int
+        L.qhuff_svc_open.argtypes = [vp, C.c_uint, C.c_uint,
+                                     C.POINTER(C.c_void_p)]
+        L.qhuff_svc_close.restype = None
+        L.qhuff_svc_close.argtypes = [vp]
+        L.qhuff_svc_encode.restype = C.c_int
+        L.qhuff_svc_encode.argtypes = [vp, vp, u32p, C.c_uint32, C.c_uint, vp,
+                                       u32p]
+        L.qhuff_svc_decode.restype = C.c_int
+        L.qhuff_svc_decode.argtypes = [vp, vp, u32p, C.c_uint32, vp, u32p, vp]
+        L.qhuff_svc_stats.restype = C.c_int
+        L.qhuff_svc_stats.argtypes = [vp, C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64)]
         L.qhuff_frame_literal.restype = C.c_int
         L.qhuff_frame_literal.argtypes = [C.c_uint, vp, C.c_size_t,
                                           C.c_char_p, C.c_uint, C.c_char_p,
@@ -301,6 +317,9 @@ class Codec:
 
     def close(self):
         if self._ctx:
+            svc = getattr(self, "_service", None)
+            if svc is not None:
+                svc._svc = C.c_void_p()      # qhuff_close frees it
             lib().qhuff_close(self._ctx)
             self._ctx = C.c_void_p()
 
@@ -478,6 +497,11 @@ class Codec:
         return ([out[out_off[i]:out_off[i + 1]].tobytes() for i in range(n)],
                 status[:n])
 
+    def service(self, slots=0, idle_us=0):
+        """Attach the low-latency service (qhuff_svc_open) -> Service."""
+        self._service = Service(self, slots, idle_us)
+        return self._service
+
     # per-string mirrors of the reference entry points ----------------------
     def enc_enc_str(self, prefix_bits, s, first_byte=0, dst_len=1 << 20):
         buf = C.create_string_buffer(max(dst_len, 1))
@@ -500,3 +524,80 @@ class Codec:
         rv = lib().qhuff_huff_decode_ex(self._ctx, s, len(src), d, dst_len,
                                         C.byref(st), final)
         return rv.status, d.raw[:rv.n_dst], rv.n_src
+
+
+class Service:
+    """The resident low-latency service on a Codec's context (qhuff_svc_*):
+    small host-memory batches without a kernel launch per call.  While it is
+    open, the context's own host-path calls that fit a slot use it too."""
+
+    def __init__(self, codec, slots=0, idle_us=0):
+        self.codec = codec                   # keeps the context alive
+        self._svc = C.c_void_p()
+        rc = lib().qhuff_svc_open(codec._ctx, slots, idle_us,
+                                  C.byref(self._svc))
+        if rc != OK:
+            err = lib().qhuff_last_error(codec._ctx)
+            raise QhuffError("qhuff_svc_open failed: %d (%s)" % (
+                rc, err.decode() if err else ""))
+
+    def close(self):
+        if self._svc:
+            lib().qhuff_svc_close(self._svc)
+            self._svc = C.c_void_p()
+        if getattr(self.codec, "_service", None) is self:
+            self.codec._service = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc != OK:
+            err = lib().qhuff_last_error(self.codec._ctx)
+            raise QhuffError("%s failed: %d (%s)" % (what, rc,
+                             err.decode() if err else ""))
+
+    def stats(self):
+        """(calls served by the kernel, kernel launches, calls sent to the
+        host path)"""
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._check(lib().qhuff_svc_stats(self._svc, C.byref(a), C.byref(b),
+                                          C.byref(c)), "qhuff_svc_stats")
+        return a.value, b.value, c.value
+
+    def encode(self, data, in_off, mode=ENC_PAYLOAD, out=None, out_off=None):
+        import numpy as np
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
+        n = len(in_off) - 1
+        if out is None:
+            out = np.zeros(encode_bound(int(in_off[-1] - in_off[0]), n, mode),
+                           dtype=np.uint8)
+        if out_off is None:
+            out_off = np.zeros(n + 1, dtype=np.uint32)
+        self._check(lib().qhuff_svc_encode(self._svc, _np_ptr(data),
+                                           _np_ptr(in_off), n, mode,
+                                           _np_ptr(out), _np_ptr(out_off)),
+                    "qhuff_svc_encode")
+        return out[:out_off[-1]], out_off
+
+    def decode(self, data, in_off, out=None, out_off=None, status=None):
+        import numpy as np
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
+        n = len(in_off) - 1
+        if out is None:
+            out = np.zeros(decode_bound(int(in_off[-1] - in_off[0]), n),
+                           dtype=np.uint8)
+        if out_off is None:
+            out_off = np.zeros(n + 1, dtype=np.uint32)
+        if status is None:
+            status = np.zeros(max(n, 1), dtype=np.uint8)
+        self._check(lib().qhuff_svc_decode(self._svc, _np_ptr(data),
+                                           _np_ptr(in_off), n, _np_ptr(out),
+                                           _np_ptr(out_off), _np_ptr(status)),
+                    "qhuff_svc_decode")
+        return out[:out_off[-1]], out_off, status[:n]

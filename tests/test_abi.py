@@ -44,7 +44,7 @@ def test_library_has_gfx950_code_object():
 def test_header_is_plain_c():
     """The boundary headers must compile as C99 with no HIP/torch types."""
     src = "".join('#include "%s"\n' % h for h in qhuff.HEADERS) + \
-        "int main(void){return QHUFF_ABI_VERSION != 2;}\n"
+        "int main(void){return QHUFF_ABI_VERSION != 3;}\n"
     r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-x", "c",
                         "-fsyntax-only", "-"], input=src, text=True,
                        capture_output=True)
@@ -114,11 +114,25 @@ def test_shard_cuts_balance():
 
 def test_abi_version_matches_header():
     """the loaded library reports the header's QHUFF_ABI_VERSION (no device
-    needed); ABI 2 keeps version 1's 5-argument qhuff_huff_decode beside
-    qhuff_huff_decode_ex"""
-    assert qhuff.lib().qhuff_abi_version() == 2
+    needed); ABI 2 kept version 1's 5-argument qhuff_huff_decode beside
+    qhuff_huff_decode_ex; ABI 3 adds the qhuff_svc_* service
+    and keeps every earlier entry point"""
+    assert qhuff.lib().qhuff_abi_version() == 3
     src = open(os.path.join(ROOT, "include", "qhuff.h")).read()
-    assert "#define QHUFF_ABI_VERSION 2" in src
+    assert "#define QHUFF_ABI_VERSION 3" in src
     assert "qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, " \
            "int src_len,\n                  unsigned char *dst, int dst_len);" \
         in src
+
+
+def test_service_entry_points_reject_null():
+    """qhuff_svc_* with no context / service: QHUFF_EINVAL, no device touched"""
+    L = qhuff.lib()
+    p = C.c_void_p()
+    assert L.qhuff_svc_open(None, 0, 0, C.byref(p)) == qhuff.EINVAL
+    assert not p.value
+    assert L.qhuff_svc_encode(None, None, None, 0, 0, None, None) == qhuff.EINVAL
+    assert L.qhuff_svc_decode(None, None, None, 0, None, None, None) == \
+        qhuff.EINVAL
+    assert L.qhuff_svc_stats(None, None, None, None) == qhuff.EINVAL
+    L.qhuff_svc_close(None)
