@@ -15,9 +15,10 @@
  *
  * Each call codes one string on the calling thread's default context (opened
  * on first use on qhuff_lsqpack_set_device()'s device, else $QHUFF_DEVICE,
- * else the current HIP device).  The per-string path pays a launch and two
- * PCIe copies per call: it is the drop-in, the batch calls in qhuff.h are the
- * fast path.
+ * else the current HIP device), or on the context qhuff_lsqpack_set_context
+ * shares.  Without a service attached a call pays a launch and two PCIe
+ * copies; with one (qhuff_svc_open on a shared context) it is one request to
+ * the resident kernel.  The batch calls in qhuff.h are the fast path.
  */
 #ifndef QHUFF_LSQPACK_H
 #define QHUFF_LSQPACK_H 1
@@ -72,6 +73,13 @@ void qhuff_lsqpack_set_decode_full(qhuff_huff_decode_full_fn fn);
 /* Device of the calling thread's default context (before its first call;
  * QHUFF_EINVAL after).  Returns QHUFF_OK. */
 int qhuff_lsqpack_set_device(int device);
+
+/* Serve every thread's calls from one context instead of a default context
+ * per thread (NULL: back to those).  The context must have the low-latency
+ * service attached (qhuff_svc_open): it makes these one-string calls
+ * thread-safe and answers them without a kernel launch per call.  The
+ * caller keeps ctx open while it is set.  Returns QHUFF_OK. */
+int qhuff_lsqpack_set_context(qhuff_ctx *ctx);
 
 #ifdef __cplusplus
 }

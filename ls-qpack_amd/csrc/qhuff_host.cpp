@@ -920,7 +920,20 @@ struct qhuff_svc
     std::mutex launch_mu;            // (re)launch of the kernel
     std::mutex fallback_mu;          // large requests: the context's host path
     std::atomic<uint64_t> served{0}, launches{0}, fallbacks{0};
+    // steady-clock ns of the last answered request: within idle_us / 2 of
+    // it the kernel cannot have left for idle, and a call skips the stream
+    // query (a lock in the HIP runtime every caller would queue on)
+    std::atomic<int64_t> last_done_ns{0};
+    int64_t fresh_ns;
 };
+
+static inline int64_t
+steady_ns()
+{
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 static inline SvcHdr *
 svc_hdr(qhuff_svc *v, uint32_t k)
@@ -986,6 +999,7 @@ qhuff_svc_open(qhuff_ctx *c, unsigned slots, unsigned idle_us, qhuff_svc **out)
     v->grid = grid;
     v->n_slots = grid * wpb;
     v->idle_ticks = 100ull * (idle_us ? idle_us : 20000u);   // 100 MHz clock
+    v->fresh_ns = 500ll * (idle_us ? idle_us : 20000u);      // idle_us / 2
     v->life_ticks = 100ull * 1000000ull * 10;                // 10 s
     v->busy = new std::atomic<uint32_t>[v->n_slots];
     v->seq = new uint32_t[v->n_slots];
@@ -1113,10 +1127,9 @@ svc_post(qhuff_svc *v, uint32_t k, bool enc, const uint8_t *in,
         so[i] = in_off[s0 + i] - a0;
     if (nb)
         memcpy(sb + kSvcInAt, in + a0, nb);
-    h->op = enc ? kSvcOpEncode : kSvcOpDecode;
     h->n = n;
-    h->mode = mode;
     h->in_bytes = nb;
+    h->opmode = (enc ? kSvcOpEncode : kSvcOpDecode) | (mode << 8);
     const uint32_t sq = v->seq[k] + 1 ? v->seq[k] + 1 : 1;
     v->seq[k] = sq;
     __atomic_store_n(&h->req, sq, __ATOMIC_RELEASE);
@@ -1229,7 +1242,10 @@ svc_call(qhuff_svc *v, bool enc, const uint8_t *in, const uint32_t *in_off,
             p0[++np] = s1;
             s0 = s1;
         }
-        int rc = svc_ensure_running(v);
+        int rc = QHUFF_OK;
+        if (steady_ns() - v->last_done_ns.load(std::memory_order_relaxed)
+                > v->fresh_ns)
+            rc = svc_ensure_running(v);
         for (uint32_t j = 0; j < np && !rc; ++j)
         {
             rc = svc_wait(v, slot[j], sq[j]);
@@ -1246,6 +1262,7 @@ svc_call(qhuff_svc *v, bool enc, const uint8_t *in, const uint32_t *in_off,
     }
     out_off[n] = base;
     v->served.fetch_add(1, std::memory_order_relaxed);
+    v->last_done_ns.store(steady_ns(), std::memory_order_relaxed);
     return QHUFF_OK;
 }
 

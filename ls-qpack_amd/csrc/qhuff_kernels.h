@@ -98,12 +98,14 @@ constexpr uint32_t kSvcOpEncode = 1;
 
 struct SvcHdr
 {
+    // the request's first 16 bytes are read by one 16-byte load per poll:
+    // the host writes n, in_bytes and opmode, then req (release), all in one
+    // cache line, so a load that sees the new req sees the fields too
     uint32_t req;                // host: sequence of the posted request (last)
-    uint32_t op;                 // kSvcOpDecode / kSvcOpEncode
     uint32_t n;                  // strings
-    uint32_t mode;               // encode mode
     uint32_t in_bytes;
-    uint32_t pad0[27];           // (the device's words on their own line)
+    uint32_t opmode;             // kSvcOp* | encode mode << 8
+    uint32_t pad0[28];           // (the device's words on their own line)
     uint32_t done;               // device: sequence of the last served request
     uint32_t total;              // device: its output bytes
     uint32_t pad1[30];

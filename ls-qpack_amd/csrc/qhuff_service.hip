@@ -53,6 +53,20 @@ sys_load(const uint32_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// a slot header's first 16 bytes in one system-coherent load (sc0 sc1: past
+// the caches, as the system-scope atomic loads are), waited for
+__device__ __forceinline__ u32x4
+poll_hdr(const SvcHdr *h)
+{
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\t"
+                 "s_waitcnt vmcnt(0)"
+                 : "=v"(v)
+                 : "v"(h)
+                 : "memory");
+    return v;
+}
+
 // 16-byte chunks [0, na) of region a, then [0, nb) of region b, from src
 // to dst (two regions of the slot layout, in one pass: one memory round
 // trip for up to 8 chunks per lane)
@@ -177,9 +191,11 @@ qhuff_service_kernel(SvcArgs a)
     // a request posted while no service ran (req != done) is served first
     uint32_t last = __builtin_amdgcn_readfirstlane(sys_load(&h->done));
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;)
+    for (uint32_t it = 0;; ++it)
     {
-        const uint32_t req = __builtin_amdgcn_readfirstlane(sys_load(&h->req));
+        // one PCIe round trip per poll: the request word and its fields
+        const u32x4 hd = poll_hdr(h);
+        const uint32_t req = __builtin_amdgcn_readfirstlane(hd.x);
         if (req != last)
         {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -187,11 +203,10 @@ qhuff_service_kernel(SvcArgs a)
                 __hip_atomic_fetch_max((unsigned long long *) a.active,
                                        (unsigned long long) __builtin_amdgcn_s_memrealtime(),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t op = __builtin_amdgcn_readfirstlane(sys_load(&h->op));
-            const uint32_t n = __builtin_amdgcn_readfirstlane(sys_load(&h->n));
-            const uint32_t mode = __builtin_amdgcn_readfirstlane(sys_load(&h->mode));
-            const uint32_t in_bytes =
-                __builtin_amdgcn_readfirstlane(sys_load(&h->in_bytes));
+            const uint32_t n = __builtin_amdgcn_readfirstlane(hd.y);
+            const uint32_t in_bytes = __builtin_amdgcn_readfirstlane(hd.z);
+            const uint32_t op = __builtin_amdgcn_readfirstlane(hd.w) & 0xff;
+            const uint32_t mode = __builtin_amdgcn_readfirstlane(hd.w) >> 8;
             // (the host checks n, in_bytes and the offsets; these bounds only
             // keep a corrupt slot inside its own memory)
             const uint32_t nn = n < kSvcMaxStrings ? n : kSvcMaxStrings;
@@ -256,6 +271,7 @@ qhuff_service_kernel(SvcArgs a)
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             last = req;
+            it = 0;
             continue;
         }
         // Leaving: the waves of a workgroup leave together (a wave that left
@@ -266,6 +282,8 @@ qhuff_service_kernel(SvcArgs a)
         // finds the service stream idle).
         if (__builtin_amdgcn_readfirstlane(*(volatile QH_LDS uint32_t *) &sm->quit))
             break;
+        if (it % 16 != 15)                   // stop word and clock: every 16th
+            continue;
         if (__builtin_amdgcn_readfirstlane(sys_load(&a.ctl[0])))
             break;
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -278,7 +296,6 @@ qhuff_service_kernel(SvcArgs a)
             *(volatile QH_LDS uint32_t *) &sm->quit = 1;
             break;
         }
-        __builtin_amdgcn_s_sleep(4);
     }
 }
 

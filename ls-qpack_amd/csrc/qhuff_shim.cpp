@@ -27,6 +27,8 @@
 namespace {
 
 std::atomic<qhuff_huff_decode_full_fn> g_full{nullptr};
+// a context shared by every thread (qhuff_lsqpack_set_context)
+std::atomic<qhuff_ctx *> g_shared{nullptr};
 
 // the calling thread's default context (closed at thread exit)
 struct ThreadCtx
@@ -46,6 +48,8 @@ thread_local ThreadCtx t_ctx;
 qhuff_ctx *
 default_ctx()
 {
+    if (qhuff_ctx *s = g_shared.load(std::memory_order_acquire))
+        return s;
     if (!t_ctx.ctx)
     {
         int dev = t_ctx.device;
@@ -184,5 +188,12 @@ qhuff_lsqpack_set_device(int device)
     if (t_ctx.ctx)
         return QHUFF_EINVAL;
     t_ctx.device = device;
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_lsqpack_set_context(qhuff_ctx *ctx)
+{
+    g_shared.store(ctx, std::memory_order_release);
     return QHUFF_OK;
 }

@@ -38,6 +38,7 @@ EXPORTS = (
     # include/qhuff_lsqpack.h
     "qhuff_lsqpack_enc_enc_str", "qhuff_lsqpack_huff_decode",
     "qhuff_lsqpack_set_decode_full", "qhuff_lsqpack_set_device",
+    "qhuff_lsqpack_set_context",
 )
 EPROTO, ETRUNC = -71, -61
 LIT_NAME, LIT_VALUE = 1, 2
@@ -136,6 +137,8 @@ def lib():
                                                 C.c_int]
         L.qhuff_lsqpack_set_decode_full.restype = None
         L.qhuff_lsqpack_set_decode_full.argtypes = [C.c_void_p]
+        L.qhuff_lsqpack_set_context.restype = C.c_int
+        L.qhuff_lsqpack_set_context.argtypes = [C.c_void_p]
         L.qhuff_lsqpack_set_device.restype = C.c_int
         L.qhuff_lsqpack_set_device.argtypes = [C.c_int]
         L.qhuff_last_error.restype = C.c_char_p

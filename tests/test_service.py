@@ -225,3 +225,37 @@ def test_svc_routes_context_host_calls(codec, svc):
     st, dst, n_src = codec.huff_decode(O.huffman_enc(b"text/html"))[:3]
     assert st == 0 and dst == b"text/html"
     assert svc.stats()[0] >= served0 + 6
+
+
+def test_svc_shared_context_for_lsqpack_shims(codec, svc):
+    """qhuff_lsqpack_set_context: the reference-signature per-string calls of
+    several threads on one context with the service attached"""
+    import qhuff
+    L = qhuff.lib()
+    served0 = svc.stats()[0]
+    assert L.qhuff_lsqpack_set_context(codec._ctx) == qhuff.OK
+    errors = []
+
+    def worker(t):
+        try:
+            rng = random.Random(t)
+            for _ in range(40):
+                s = bytes(rng.choice(b"abcdefgh-./:0123") for _ in
+                          range(rng.randint(0, 60)))
+                assert qhuff.lsqpack_enc_enc_str(5, s) == O.enc_enc_str(5, s)
+                h = O.huffman_enc(s)
+                st, dst = qhuff.lsqpack_huff_decode(h, len(s) + 1)[:2]
+                assert st == 0 and dst == s
+        except Exception as e:                      # noqa: BLE001
+            errors.append(repr(e))
+
+    try:
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+    finally:
+        L.qhuff_lsqpack_set_context(None)
+    assert not errors, errors[:3]
+    assert svc.stats()[0] >= served0 + 4 * 40 * 2

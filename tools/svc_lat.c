@@ -5,10 +5,12 @@
  * and the per-string entry point qhuff_enc_enc_str with and without a
  * service attached.  Prints one JSON object.
  *
- * build: gcc -O2 -std=c11 -I include tools/svc_lat.c -o tools/svc_lat \
- *            -L ls-qpack_amd -lqhuff -Wl,-rpath,$PWD/ls-qpack_amd
+ * build: gcc -O2 -std=c11 -pthread -I include tools/svc_lat.c \
+ *            -o tools/svc_lat -L ls-qpack_amd -lqhuff \
+ *            -Wl,-rpath,'$ORIGIN/../ls-qpack_amd' 
  * usage: tools/svc_lat [calls] */
 #define _POSIX_C_SOURCE 199309L
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -60,6 +62,34 @@ put(const char *name, struct stat3 s, int last)
             exit(1);                                                         \
         }                                                                    \
     } while (0)
+
+/* throughput: T threads each encoding header blocks through the service */
+struct tp_arg
+{
+    qhuff_svc *svc;
+    const uint8_t *data;
+    const uint32_t *off;
+    uint32_t n;
+    double secs;
+    long calls;
+};
+
+static void *
+tp_worker(void *p)
+{
+    struct tp_arg *a = p;
+    uint8_t out[8192];
+    uint32_t oo[65];
+    const double t0 = now_us();
+    long k = 0;
+    while (now_us() - t0 < a->secs * 1e6)
+    {
+        CHK(qhuff_svc_encode(a->svc, a->data, a->off, a->n, 0, out, oo));
+        ++k;
+    }
+    a->calls = k;
+    return NULL;
+}
 
 int
 main(int argc, char **argv)
@@ -143,6 +173,33 @@ main(int argc, char **argv)
         printf("}");
         free(data), free(off), free(enc), free(dec), free(st), free(eoff);
         free(doff), free(huff), free(hoff);
+    }
+    {
+        /* 20-string header blocks from T threads for 0.5 s each */
+        uint8_t data[64 * 20 + 64];
+        uint32_t off[21];
+        qhuff_synth_batch(77, 20, 8, 64, (const uint8_t *) "abcdefghij-./", 13,
+                          data, off);
+        printf("}, \"threads_header_block_encode\": {");
+        const int ts[] = {1, 2, 4, 8, 12, 16};
+        for (unsigned j = 0; j < sizeof(ts) / sizeof(ts[0]); ++j)
+        {
+            pthread_t th[16];
+            struct tp_arg ar[16];
+            for (int i = 0; i < ts[j]; ++i)
+            {
+                ar[i] = (struct tp_arg){svc, data, off, 20, 0.5, 0};
+                pthread_create(&th[i], NULL, tp_worker, &ar[i]);
+            }
+            long tot = 0;
+            for (int i = 0; i < ts[j]; ++i)
+            {
+                pthread_join(th[i], NULL);
+                tot += ar[i].calls;
+            }
+            printf("%s\"%d\": {\"blocks_per_s\": %.0f, \"strings_per_s\": %.0f}",
+                   j ? ", " : "", ts[j], tot / 0.5, 20 * tot / 0.5);
+        }
     }
     uint64_t served, launches, fb;
     qhuff_svc_stats(svc, &served, &launches, &fb);
