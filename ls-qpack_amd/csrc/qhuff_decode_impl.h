@@ -272,7 +272,10 @@ decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
 // live in the rare long-code branch.  The last < kWinBits bits (at most two
 // symbols) take the padded epilogue with the D3 tail rule, exactly as
 // decode_string().
-template <class Emit>
+// R2: two main steps per loop trip share one refill read of the next input
+// dword (step lab at 12 waves/CU: 8,633 vs 9,795 cycles per tile; decode
+// 62.7 vs 64.0 us in-process, profiles/r03_p); false: one read per step.
+template <class Emit, bool R2 = true>
 __device__ __forceinline__ int
 decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
                   const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
@@ -330,9 +333,27 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
             emit(e, ent_ns(e));
             rem -= c;
             advance(c);
-            nx = src[p];
+            if constexpr (!R2)
+                nx = src[p];
             W = __builtin_amdgcn_alignbit(A, B, t);
             idx = win_addr(W, rem >= kMain);
+            if constexpr (R2)
+            {
+                // A second step on the same refill: a main step consumes at
+                // most 13 bits, and a step that moves the window on a dword
+                // leaves t >= 19, so the two steps cross at most one dword
+                // boundary and the next dword nx read before them covers it.
+                // (A lane that stalled or went on hold in the first step
+                // reads the same entry again and consumes nothing.)
+                e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
+                const uint32_t c2 = ent_c(e);
+                emit(e, ent_ns(e));
+                rem -= c2;
+                advance(c2);
+                nx = src[p];
+                W = __builtin_amdgcn_alignbit(A, B, t);
+                idx = win_addr(W, rem >= kMain);
+            }
         } while (__builtin_amdgcn_ballot_w64((rem >= kMain) & (e >= (1u << 24))));
         // lanes left with >= kMain bits sit on a code of 14..30 bits; EOS,
         // or a code running past the end, rejects the string (D3)

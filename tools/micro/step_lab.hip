@@ -152,6 +152,15 @@ lab(DecArgs a, int reps, MbOut *res)
             U16Emit em{wv->arena + sl, wv->arena + sl, 0};
             n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em);
         }
+        else if (MODE == 9 || MODE == 10)
+        {
+            // the kernel's sink (fixed stride 108), one refill read per step
+            // (9) or per two steps (10, QH_REFILL2)
+            ArenaEmit em{wv->arena + 108 * lane, wv->arena + 108 * lane, 0};
+            n = MODE == 9
+                ? decode_string_lds<ArenaEmit, false>(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em)
+                : decode_string_lds<ArenaEmit, true>(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+        }
         else
         {
             // the kernel's two byte stores into a fixed-stride lane-major
@@ -349,6 +358,20 @@ int main(int argc, char **argv)
     DecArgs a = {};
     a.in = d_h; a.in_off = d_ho; a.win = d_win; a.sorted = d_sorted; a.n = n;
     a.c.n_tiles = n / 64;
+    if (argc > 2)
+    {
+        // the refill A/B only, interleaved
+        for (int k = 0; k < 3; ++k)
+        {
+            run<1, 9>("fixed108 r1", a, reps);
+            run<1, 10>("fixed108 r2", a, reps);
+            run<8, 9>("fixed108 r1", a, reps);
+            run<8, 10>("fixed108 r2", a, reps);
+            run<12, 9>("fixed108 r1", a, reps);
+            run<12, 10>("fixed108 r2", a, reps);
+        }
+        return 0;
+    }
     run<1, 0>("arena b8x2", a, reps);
     run<4, 0>("arena b8x2", a, reps);
     run<8, 0>("arena b8x2", a, reps);

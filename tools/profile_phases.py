@@ -116,6 +116,13 @@ def report(tag, p):
         print("  iter %2d: waves %5d  start p50 %8.0f max %8.0f   end p50 %8.0f max %8.0f"
               % (it, ok.sum(), np.median(s), s.max(),
                  np.median(e) if e.size else 0, e.max() if e.size else 0))
+        # this iteration's phases (mean cycles), same order as above
+        ph = []
+        for k in range(6):
+            a, b = p[ok, it, k], p[ok, it, k + 1]
+            g = (a != 0) & (b != 0)
+            ph.append((b - a)[g].mean() if g.any() else 0.0)
+        print("           phases " + " ".join("%6.0f" % x for x in ph))
 
 
 def slow_report(p, live):
