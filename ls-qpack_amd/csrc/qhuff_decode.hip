@@ -25,6 +25,11 @@
 // the look-back has resolved the tile's output base.
 #include "qhuff_decode_impl.h"
 
+// tickets claimed per wave in the prologue, at most (tile_pipeline)
+#ifndef QH_DEC_PER
+#define QH_DEC_PER 3
+#endif
+
 namespace qhuff {
 
 using DecPolicy = DecPolicyT<DecSmem>;
@@ -38,23 +43,34 @@ qhuff_decode_kernel(DecArgs a)
     prof_realtime(a.c, kProfIters - 1, 10);      // (profiling) wave entry
     Tickets tk;
     tk.init();
-    {
-        // every load of the tables issued before the first LDS store (one
-        // memory round trip, not one per loop trip), the ticket claims
-        // beside them
-        constexpr int kPer = (kWinSize / 4 + 64 * kWaves - 1) / (64 * kWaves);
-        const QH_GLB u32x4 *gw = (const QH_GLB u32x4 *) glb(a.win);
-        QH_LDS u32x4 *sw = (QH_LDS u32x4 *) sm->win;
-        u32x4 v[kPer];
+    // The workgroup's ticket claims go out first, then every load of the
+    // tables; the claims are waited for (not the tables) and shared at the
+    // first barrier, each wave then issues its first offsets loads, and only
+    // then are the tables stored and the second barrier passed (in
+    // tile_pipeline's mid()): the offsets loads overlap the table loads.
+    const uint32_t cb = claim_block_issue(a.c, tk, QH_DEC_PER);
+    constexpr int kPer = (kWinSize / 4 + 64 * kWaves - 1) / (64 * kWaves);
+    const QH_GLB u32x4 *gw = (const QH_GLB u32x4 *) glb(a.win);
+    u32x4 v[kPer];
 #pragma unroll
-        for (int r = 0; r < kPer; ++r)
-        {
-            const int i = tid + r * 64 * kWaves;
-            v[r] = gw[i < kWinSize / 4 ? i : 0];
-        }
-        const QH_GLB uint16_t *gs = glb(a.sorted);
-        const uint16_t so = gs[tid < 257 ? tid : 0];
-        claim_block_tickets(a.c, tk, &sm->tk);
+    for (int r = 0; r < kPer; ++r)
+    {
+        const int i = tid + r * 64 * kWaves;
+        v[r] = gw[i < kWinSize / 4 ? i : 0];
+    }
+    const QH_GLB uint16_t *gs = glb(a.sorted);
+    const uint16_t so = gs[tid < 257 ? tid : 0];
+    claim_block_store(a.c, cb, &sm->tk, QH_DEC_PER);
+    clear_next_launch(a.c);
+    // the tickets: LDS stores visible, no wait for the table loads (a
+    // __syncthreads() would drain them)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
+    DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
+    uint32_t k0, k1, k2;
+    wave_tickets(tk, &sm->tk, &k0, &k1, &k2);
+    auto tables = [&]() {
+        QH_LDS u32x4 *sw = (QH_LDS u32x4 *) sm->win;
 #pragma unroll
         for (int r = 0; r < kPer; ++r)
         {
@@ -66,15 +82,10 @@ qhuff_decode_kernel(DecArgs a)
             sm->sorted[tid] = so;
         if (tid == 0)
             sm->win[kHoldIdx] = kHoldEntry;
-        clear_next_launch(a.c);
-    }
-    __syncthreads();                 // the only workgroup barrier
-    prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
-    DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
-    uint32_t k0, k1;
-    wave_tickets(tk, &sm->tk, &k0, &k1);
-    tile_pipeline(pol, a.c, tk, k0, k1, a.in, a.in_off,
-                  a.n, a.out, a.out_off, a.status);
+        __syncthreads();             // the tables
+    };
+    tile_pipeline(pol, a.c, tk, k0, k1, k2, a.in, a.in_off,
+                  a.n, a.out, a.out_off, a.status, tables);
 }
 
 hipError_t

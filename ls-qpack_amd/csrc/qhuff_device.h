@@ -226,8 +226,12 @@ __device__ __forceinline__ void
 clear_next_launch(const Coord &c)
 {
     const uint32_t par = (c.epoch + 1) & 1;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < c.cap_super;
-         i += gridDim.x * blockDim.x)
+    // (the workgroup size as the constant it is: blockDim.x is a vector
+    // load from the dispatch packet, and its wait drained every load and
+    // atomic of the prologue)
+    constexpr uint32_t kBT = 64u * kWaves;
+    for (uint32_t i = blockIdx.x * kBT + threadIdx.x; i < c.cap_super;
+         i += gridDim.x * kBT)
         __hip_atomic_store(&c.sacc[((uint64_t) par * c.cap_super + i) * kAccStride], 0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0 && threadIdx.x < kTickGroups)
@@ -292,7 +296,7 @@ prof_value(const Coord &c, uint32_t it, int ph, uint64_t v)
 #ifdef QHUFF_PROFILE
     if (c.prof && it < (uint32_t) kProfIters && (threadIdx.x & 63) == 0)
     {
-        const uint64_t gid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        const uint64_t gid = blockIdx.x * (uint64_t) kWaves + (threadIdx.x >> 6);
         c.prof[(gid * kProfIters + it) * kProfSlots + ph] = v;
     }
 #else

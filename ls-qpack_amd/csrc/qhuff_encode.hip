@@ -31,6 +31,11 @@
 // (global reads / per-lane global writes).
 #include "qhuff_encode_impl.h"
 
+// tickets claimed per wave in the prologue, at most (tile_pipeline)
+#ifndef QH_ENC_PER
+#define QH_ENC_PER 2
+#endif
+
 namespace qhuff {
 
 using EncPolicy = EncPolicyT<EncSmem>;
@@ -45,7 +50,7 @@ qhuff_encode_kernel(EncArgs a)
     clear_next_launch(a.c);
     Tickets tk;
     tk.init();
-    claim_block_tickets(a.c, tk, &sm->tk);
+    claim_block_tickets(a.c, tk, &sm->tk, QH_ENC_PER);
     __syncthreads();                 // the only workgroup barrier
     EncPolicy pol;
     pol.in = a.in;
@@ -53,9 +58,9 @@ qhuff_encode_kernel(EncArgs a)
     pol.sm = sm;
     pol.wv = &sm->w[tid >> 6];
     pol.dense = false;
-    uint32_t k0, k1;
-    wave_tickets(tk, &sm->tk, &k0, &k1);
-    tile_pipeline(pol, a.c, tk, k0, k1, a.in, a.in_off,
+    uint32_t k0, k1, k2;
+    wave_tickets(tk, &sm->tk, &k0, &k1, &k2);
+    tile_pipeline(pol, a.c, tk, k0, k1, k2, a.in, a.in_off,
                   a.n, a.out, a.out_off, nullptr);
 }
 

@@ -130,25 +130,28 @@ wait_vm_all()
     __builtin_amdgcn_s_waitcnt(0x0f70);
 }
 
-// The kernel prologue claims the first two tickets of every wave of the
+// The kernel prologue claims the first tickets of every wave of the
 // workgroup: lanes 0..kTickGroups-1 of the first wave each take one group's
 // share with one returning atomic (~3,000 waves claiming one by one would
 // queue on the counters).  A wave of group g that is the r-th of its group
-// in the workgroup gets tickets base + r and base + n_g + r (n_g waves of
-// the workgroup in group g).  The second tickets only when the grid's first
-// claims cannot cover every tile (a small batch then gets one tile per wave,
-// not two per wave of the first workgroups to start); otherwise kClaimNow:
-// the wave claims its second ticket itself once it runs, like every later
-// one (a second tile fixed to whichever workgroup claimed it would need the
-// whole grid resident: with only some workgroups resident, e.g. beside
-// another context, a group's tickets could run ahead of another's and the
-// look-backs above the gap wait for tiles no running wave can claim).
-constexpr uint32_t kClaimNow = 0xffffffffu;   // second ticket: claim it in
-                                              // the wave (tile_pipeline)
+// in the workgroup gets tickets base + r, base + n_g + r and base + 2 n_g + r
+// (n_g waves of the workgroup in group g).  Three tickets per wave when the
+// tiles cover three per wave of the whole grid (the third replaces the
+// wave's own first claim, whose burst of ~3,000 returning adds the first
+// iteration would wait for), two when they cover two, else one (a small
+// batch then gets one tile per wave, not several per wave of the first
+// workgroups to start); a ticket not claimed here is kClaimNow: the wave
+// claims it itself once it runs, like every later one (a tile fixed to
+// whichever workgroup claimed it would need the whole grid resident: with
+// only some workgroups resident, e.g. beside another context, a group's
+// tickets could run ahead of another's and the look-backs above the gap
+// wait for tiles no running wave can claim).
+constexpr uint32_t kClaimNow = 0xffffffffu;   // ticket: claim it in the wave
+                                              // (tile_pipeline)
 struct BlockTickets
 {
     uint32_t base[kTickGroups];
-    uint32_t two;                    // second tickets claimed
+    uint32_t per;                    // tickets claimed per wave (1..3)
 };
 
 __device__ __forceinline__ uint32_t
@@ -161,51 +164,94 @@ tick_group_waves(uint32_t q)
          ? ((uint32_t) kWaves - 1 - first) / kTickGroups + 1 : 0u;
 }
 
-__device__ __forceinline__ void
-claim_block_tickets(const Coord &c, const Tickets &tk, QH_LDS BlockTickets *bt)
+// tickets claimed per wave in the prologue
+__device__ __forceinline__ uint32_t
+block_claims_per_wave(const Coord &c, uint32_t maxper)
+{
+    const uint64_t g = (uint64_t) gridDim.x * kWaves;
+    return (uint64_t) c.n_tiles >= 3 * g && maxper >= 3 ? 3u
+         : (uint64_t) c.n_tiles > g ? 2u : 1u;
+}
+
+// the atomic of this thread's group share (threads 0..kTickGroups-1; its
+// value is waited for only where it is stored: claim_block_store)
+__device__ __forceinline__ uint32_t
+claim_block_issue(const Coord &c, const Tickets &tk, uint32_t maxper)
 {
     const uint32_t t = threadIdx.x;
-    const bool two = (uint64_t) c.n_tiles > (uint64_t) gridDim.x * kWaves;
+    uint32_t b = 0;
     if (t < kTickGroups)
     {
         const uint32_t nq = tick_group_waves(t);
-        uint32_t b = 0;
         if (nq)
-            b = __hip_atomic_fetch_add(tk.counter(c, t), two ? 2 * nq : nq,
+            b = __hip_atomic_fetch_add(tk.counter(c, t),
+                                       block_claims_per_wave(c, maxper) * nq,
                                        __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-        bt->base[t] = b;
     }
-    if (t == 0)
-        bt->two = two ? 1u : 0u;
+    return b;
 }
 
-// this wave's first two tickets (after the workgroup barrier)
+__device__ __forceinline__ void
+claim_block_store(const Coord &c, uint32_t b, QH_LDS BlockTickets *bt,
+                  uint32_t maxper)
+{
+    const uint32_t t = threadIdx.x;
+    if (t < kTickGroups)
+        bt->base[t] = b;
+    if (t == 0)
+        bt->per = block_claims_per_wave(c, maxper);
+}
+
+__device__ __forceinline__ void
+claim_block_tickets(const Coord &c, const Tickets &tk, QH_LDS BlockTickets *bt,
+                    uint32_t maxper)
+{
+    claim_block_store(c, claim_block_issue(c, tk, maxper), bt, maxper);
+}
+
+// this wave's first tickets (after the workgroup barrier)
 __device__ __forceinline__ void
 wave_tickets(const Tickets &tk, const QH_LDS BlockTickets *bt, uint32_t *k0,
-             uint32_t *k1)
+             uint32_t *k1, uint32_t *k2)
 {
     // rank among this workgroup's waves of the same group (waves w and
     // w + kTickGroups share one)
     const uint32_t r = (threadIdx.x >> 6) / kTickGroups;
     const uint32_t nq = tick_group_waves(tk.g);
+    const uint32_t per = bt->per;
     *k0 = bt->base[tk.g] + r;
-    *k1 = bt->two ? bt->base[tk.g] + nq + r : kClaimNow;
+    *k1 = per >= 2 ? bt->base[tk.g] + nq + r : kClaimNow;
+    *k2 = per >= 3 ? bt->base[tk.g] + 2 * nq + r : kClaimNow;
 }
 
-template <class P>
+// no work between the first offsets loads and the first wait
+struct NoMid
+{
+    __device__ __forceinline__ void operator()() const {}
+};
+
+// mid(): called once by every wave after its first offsets loads have been
+// issued, before anything waits for them (the decode kernel stores its
+// window table and joins the workgroup barrier there, so the loads overlap
+// the table's); every wave of the workgroup calls it, tiles or none.
+template <class P, class Mid = NoMid>
 __device__ __forceinline__ void
 tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
-              uint32_t k1, const uint8_t *in, const uint32_t *in_off_p,
-              uint64_t n, uint8_t *out, uint32_t *out_off, uint8_t *status)
+              uint32_t k1, uint32_t k2, const uint8_t *in,
+              const uint32_t *in_off_p, uint64_t n, uint8_t *out,
+              uint32_t *out_off, uint8_t *status, Mid mid = Mid())
 {
     const QH_GLB uint32_t *in_off = (const QH_GLB uint32_t *) in_off_p;
     const uint32_t nt = c.n_tiles;
-    // tiles of this wave's first two iterations (tickets k0 < k1, claimed
-    // for the whole block in the kernel prologue)
+    // tiles of this wave's first iterations (tickets k0 < k1 < k2 claimed
+    // for the whole block in the kernel prologue, or kClaimNow)
     uint32_t t = tk.tile_of_u(k0);
     if (t >= nt)
+    {
+        mid();
         return;
+    }
     constexpr uint32_t TS = P::kTS;          // strings per tile
     auto cnt_of = [&](uint32_t tt) -> uint32_t {
         return (uint32_t) min((uint64_t) TS, n - (uint64_t) tt * TS);
@@ -227,7 +273,8 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     // tile is always coded (tickets of a group are handed out in order, so
     // once tn is past the end every later claim is too)
     const uint32_t kNone = 0xffffffffu;
-    uint32_t kq = tn < nt ? tk.claim(c) : kNone;
+    uint32_t kq = tn < nt ? (k2 == kClaimNow ? tk.claim(c) : k2) : kNone;
+    mid();
     Span sp_cur = tile_span(in, o_cur.first(), o_cur.last(), P::kInCap);
     Chunks<P::kNch> ch;
     ch.load(sp_cur);
