@@ -11,6 +11,10 @@
 #endif
 // bytes past the last slot's bound (the two-byte emitter writes one past
 // its end)
+// arena -> stage copy: compact_wave (1) or compact_string (0)
+#ifndef QH_COMPACT_WAVE
+#define QH_COMPACT_WAVE 1
+#endif
 #ifndef QH_ARENA_SLACK
 #define QH_ARENA_SLACK 16
 #endif
@@ -504,6 +508,63 @@ compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
     }
 }
 
+// The same copy for every lane of the wave at once, with whole dwords and
+// no per-dword lane branches: each lane's body dwords go out in trips of
+// eight, the trips and the dwords within them in DESCENDING order, and past
+// its last body dword a lane stores garbage instead of branching.  Lane l's
+// garbage lands only on dwords of later strings (its body starts at D_l <
+// D_m for every later lane m with a body), and lane m stores its own dword
+// X at index X - D_m < X - D_l, i.e. later in the descending order; the
+// dwords shared by two strings (heads and tails) are written byte by byte
+// after every body store.  (Each dword is its own store instruction: see
+// below.)  Garbage past the tile's last string stays below
+// the stage's end (fast tiles leave >= 64 bytes free).  One lane branch per
+// trip instead of one per dword.
+__device__ __forceinline__ void
+compact_wave(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
+{
+    uint32_t h = (4 - ((uint32_t) (uintptr_t) dstb & 3)) & 3;
+    h = h < n ? h : n;
+    const uint32_t nb = (n - h) >> 2;
+    const uint32_t nt = n - h - 4 * nb;
+    const uint32_t sa = (uint32_t) (uintptr_t) src;
+    const QH_LDS uint32_t *sw = (const QH_LDS uint32_t *) (src - (sa & 3));
+    const uint32_t s3 = sa & 3;
+    const uint32_t it = h + 4 * nb;
+    const uint32_t qt = (s3 + it) >> 2;
+    const uint32_t vh = align_bytes(sw[1], sw[0], s3);
+    const uint32_t vt = align_bytes(sw[qt + 1], sw[qt], (s3 + it) & 3);
+    const uint32_t sb = s3 + h, r = sb & 3;
+    const QH_LDS uint32_t *bw = sw + (sb >> 2);
+    QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
+    const uint32_t trips = (nb + 7) >> 3;
+    const uint32_t K = wave_max_dpp(trips);
+    for (uint32_t k = K; k-- > 0;)
+    {
+        if (k < trips)
+        {
+            uint32_t w[9];
+#pragma unroll
+            for (int j = 0; j < 9; ++j)
+                w[j] = bw[8 * k + j];
+            // one store instruction per dword, in this order: two dwords in
+            // one ds_write2 would let a lane's garbage and another lane's
+            // dword meet in one instruction (the compiler pairs neighbouring
+            // stores and may reorder them; an empty asm with a memory
+            // clobber between them stops both)
+#pragma unroll
+            for (int j = 7; j >= 0; --j)
+            {
+                dw[8 * k + j] = align_bytes(w[j + 1], w[j], r);
+                asm volatile("" ::: "memory");
+            }
+        }
+    }
+    wave_sync();
+    write_bytes(dstb, vh, h);
+    write_bytes(dstb + it, vt, nt);
+}
+
 // A tile whose input or output does not fit the stage, coded eagerly:
 // input staged -> the arena already holds the bytes (sz / st given);
 // otherwise count from global memory, then decode again to global.  The
@@ -611,9 +672,16 @@ struct DecPolicyT
     // arena -> the (dead) input stage, compacted
     __device__ __forceinline__ void emit(uint32_t excl, uint32_t sz, uint32_t)
     {
+#ifdef QH_TIME_NO_EMIT                       // timing builds only: no output
+        return;
+#endif
+#if QH_COMPACT_WAVE
+        compact_wave(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl, sz);
+#else
         if (sz)
             compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
                            sz);
+#endif
     }
 
     // a tile of the batch kernel: base from the look-back

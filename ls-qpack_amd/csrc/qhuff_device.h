@@ -180,6 +180,21 @@ wave_shr1(uint32_t v)
                                                   false);
 }
 
+// wave maximum by DPP (row shifts, then the row maxima broadcast down), in
+// every lane; VALU only
+__device__ __forceinline__ uint32_t
+wave_max_dpp(uint32_t v)
+{
+    uint32_t x = v;
+    x = max(x, dpp0<0x111, 0xf>(x));          // row_shr:1
+    x = max(x, dpp0<0x112, 0xf>(x));          // row_shr:2
+    x = max(x, dpp0<0x114, 0xf>(x));          // row_shr:4
+    x = max(x, dpp0<0x118, 0xf>(x));          // row_shr:8
+    x = max(x, dpp0<0x142, 0xa>(x));          // row_bcast:15 -> rows 1, 3
+    x = max(x, dpp0<0x143, 0xc>(x));          // row_bcast:31 -> rows 2, 3
+    return read_lane(x, 63);
+}
+
 // sum over the wave of values below 2^40 (look-back flag values): two
 // 32-bit DPP scans of the low 16 and the high 24 bits, no LDS traffic
 __device__ __forceinline__ uint64_t

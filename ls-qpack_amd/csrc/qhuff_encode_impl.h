@@ -742,6 +742,9 @@ struct EncPolicyT
         for (uint32_t i = lane_id(); i < n16; i += 64)
             o4[i] = (u32x4){0, 0, 0, 0};
         wave_sync();
+#ifdef QH_TIME_NO_EMIT                       // timing builds only: no output
+        return;
+#endif
         if (sz)
         {
             if (dense)

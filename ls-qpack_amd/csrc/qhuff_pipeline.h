@@ -273,11 +273,24 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     // tile is always coded (tickets of a group are handed out in order, so
     // once tn is past the end every later claim is too)
     const uint32_t kNone = 0xffffffffu;
-    uint32_t kq = tn < nt ? (k2 == kClaimNow ? tk.claim(c) : k2) : kNone;
+    // late: the third ticket is claimed by the wave after the first tile's
+    // input loads, and the first iteration's top does not wait for it (a
+    // burst of ~3,000 returning adds on 8 counters takes microseconds); that
+    // iteration reads it after its codec and loads the third tile's offsets
+    // then (tickets claimed by the workgroup in the prologue instead would
+    // hand each workgroup a third tile ahead of other workgroups' first and
+    // second ones, whose look-backs then wait on third tiles: profiles/r03_u)
+    const bool late = tn < nt && k1 != kClaimNow && k2 == kClaimNow;
+    uint32_t kq = tn < nt ? (k2 == kClaimNow ? 0u : k2) : kNone;
+    if (tn < nt && k2 == kClaimNow && !late)
+        kq = tk.claim(c);
     mid();
     Span sp_cur = tile_span(in, o_cur.first(), o_cur.last(), P::kInCap);
     Chunks<P::kNch> ch;
     ch.load(sp_cur);
+    if (late)
+        kq = tk.claim(c);                    // the youngest operation
+    uint32_t kq4 = 0;                        // (late) the fourth ticket
 
     // Tiles come from in-order tickets claimed two iterations ahead (one
     // claim per wave per iteration), so the order in which a wave claims
@@ -309,7 +322,11 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         // from 1.8k to 0.3k cycles but the kernels did not get faster (enc
         // 65.6 / dec 68.7 vs 65.3 / 68.3 us, interleaved A/B, profiles/r02_g)
         // -- the waves then wait longer in their look-backs.
-        wait_vm_all();
+        const bool defer = late && it == 0;  // (wave-uniform)
+        if (defer)
+            __builtin_amdgcn_s_waitcnt(0x0f71);  // all but the late claim
+        else
+            wait_vm_all();
         prof_stamp(c, it, 1);
         if (sp_cur.staged)
             pol.stage_in(ch, sp_cur, o_cur);
@@ -317,12 +334,19 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         // loads for the next tiles, a whole codec ahead of their use: input
         // of tn, offsets of the ticketed tile after it, the next ticket; the
         // oldest pending tile's look-back polls
-        const uint32_t tnn = tn < nt ? tk.tile_of(kq) : kNone;
+        uint32_t tnn = kNone;
+        if (!defer)
+            tnn = tn < nt ? tk.tile_of(kq) : kNone;
         const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), P::kInCap);
         ch.load(sp_nxt);
-        const uint32_t tz = clamp(tnn);
-        o_nn.load(in_off, (uint64_t) tz * TS, cnt_of(tz));
-        kq = tnn < nt ? tk.claim(c) : kNone;
+        if (!defer)
+        {
+            const uint32_t tz = clamp(tnn);
+            o_nn.load(in_off, (uint64_t) tz * TS, cnt_of(tz));
+            kq = tnn < nt ? tk.claim(c) : kNone;
+        }
+        else
+            kq4 = tk.claim(c);               // (past the end: never coded)
         if (pend[0].valid)
             pend[0].lb.poll(c);
         prof_stamp(c, it, 2);
@@ -366,6 +390,14 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         // the polls (a codec and an emit ago); resolve + store the oldest
         wait_vm_all();
         prof_stamp(c, it, 4);
+        if (defer)
+        {
+            // the late third ticket has landed: its tile's offsets now
+            tnn = tn < nt ? tk.tile_of(kq) : kNone;
+            const uint32_t tz = clamp(tnn);
+            o_nn.load(in_off, (uint64_t) tz * TS, cnt_of(tz));
+            kq = kq4;
+        }
         // t's add has returned with the polls: publish its super tile's
         // aggregate if that add completed it -- here, an emit after the add,
         // not at the next iteration's top (look-backs of later super tiles
