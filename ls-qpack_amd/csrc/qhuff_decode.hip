@@ -27,7 +27,7 @@
 
 // tickets claimed per wave in the prologue, at most (tile_pipeline)
 #ifndef QH_DEC_PER
-#define QH_DEC_PER 2
+#define QH_DEC_PER 3
 #endif
 
 namespace qhuff {

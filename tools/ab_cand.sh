@@ -1,10 +1,11 @@
 #!/bin/bash
 # Candidate library CAND (ls-qpack_amd/<CAND>) against BASE (default
 # libqhuff_base.so, e.g. from tools/build_rev.sh): GPU suite on the
-# candidate (QHUFF_LIB), then in-process A/Bs (tools/ab_inproc.py) in both
-# orders (the first library of a pair has shown a ~2 % encode bias).
-# Optional third argument: also the step lab's refill A/B.
-# Usage: TAG CAND [lab]
+# candidate (QHUFF_LIB; skipped with NOTEST=1), then REPS (default 3) pairs
+# of in-process A/Bs (tools/ab_inproc.py), each pair in both orders, each in
+# a fresh process (the first library's context of a process has shown a
+# 2-4 % bias, which the pairs cancel).  Optional third argument: also the
+# step lab's refill A/B.  Usage: TAG CAND [lab]
 set -e
 cd "$GRAFT_REPO_ROOT"
 o=gpurun_out/$1
@@ -17,16 +18,26 @@ if [ -z "$NOTEST" ]; then
   QHUFF_LIB=$PWD/ls-qpack_amd/$2 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $o/pytest_gpu.log 2>&1
   tail -1 $o/pytest_gpu.log
 fi
-timeout -k 10 300 python -u tools/ab_inproc.py ls-qpack_amd/$2 ls-qpack_amd/$b 20 10 > $o/ab_inproc.json
-timeout -k 10 300 python -u tools/ab_inproc.py ls-qpack_amd/$b ls-qpack_amd/$2 20 10 > $o/ab_inproc_swapped.json
+for r in $(seq 1 ${REPS:-3}); do
+  timeout -k 10 300 python -u tools/ab_inproc.py ls-qpack_amd/$2 ls-qpack_amd/$b 20 10 > $o/ab_${r}_cb.json
+  timeout -k 10 300 python -u tools/ab_inproc.py ls-qpack_amd/$b ls-qpack_amd/$2 20 10 > $o/ab_${r}_bc.json
+done
 python - $o <<'PY'
-import json, sys
+import glob, json, statistics, sys
 o = sys.argv[1]
-a = json.load(open(o + "/ab_inproc.json"))
-b = json.load(open(o + "/ab_inproc_swapped.json"))
+rat = {"enc": [], "dec": []}
+cand = {"enc": [], "dec": []}
+base = {"enc": [], "dec": []}
+for f in sorted(glob.glob(o + "/ab_*_cb.json")):
+    a = json.load(open(f))
+    b = json.load(open(f.replace("_cb.json", "_bc.json")))
+    for k in ("enc", "dec"):
+        c = (a["a_%s_med" % k] + b["b_%s_med" % k]) / 2
+        s = (a["b_%s_med" % k] + b["a_%s_med" % k]) / 2
+        cand[k].append(c); base[k].append(s); rat[k].append(c / s)
 for k in ("enc", "dec"):
-    cand = (a["a_%s_med" % k] + b["b_%s_med" % k]) / 2
-    base = (a["b_%s_med" % k] + b["a_%s_med" % k]) / 2
-    print("%s: candidate %.2f us, base %.2f us (medians, both orders), cand/base %.4f"
-          % (k, cand, base, cand / base))
+    print("%s: candidate %.2f us, base %.2f us, cand/base %.4f (pairs: %s)"
+          % (k, statistics.mean(cand[k]), statistics.mean(base[k]),
+             statistics.mean(rat[k]), " ".join("%.3f" % r for r in rat[k])))
+json.dump({"cand": cand, "base": base, "ratio": rat}, open(o + "/ab_summary.json", "w"))
 PY
