@@ -11,10 +11,6 @@
 #endif
 // bytes past the last slot's bound (the two-byte emitter writes one past
 // its end)
-// arena -> stage copy: compact_wave (1) or compact_string (0)
-#ifndef QH_COMPACT_WAVE
-#define QH_COMPACT_WAVE 1
-#endif
 #ifndef QH_ARENA_SLACK
 #define QH_ARENA_SLACK 16
 #endif
@@ -443,11 +439,7 @@ struct GlobalEmit                            // slow path: byte stores
     }
 };
 
-// arena slot -> stage at byte D (wave-synchronous; other lanes write the
-// neighbouring bytes).  Bytes up to D's dword boundary (head) and after the
-// last whole dword (tail) by byte stores, the whole dwords between from pairs
-// of aligned source words (alignbyte), four per trip with the reads of a trip
-// issued together: per trip one LDS round trip, not one per dword.
+// byte stores of the low nb (<= 3) bytes of v at d
 __device__ __forceinline__ void
 write_bytes(QH_LDS uint8_t *d, uint32_t v, uint32_t nb)
 {
@@ -459,57 +451,9 @@ write_bytes(QH_LDS uint8_t *d, uint32_t v, uint32_t nb)
         d[2] = (uint8_t) (v >> 16);
 }
 
-__device__ __forceinline__ void
-compact_string(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
-{
-    uint32_t h = (4 - ((uint32_t) (uintptr_t) dstb & 3)) & 3;
-    h = h < n ? h : n;
-    const uint32_t nb = (n - h) >> 2;
-    const uint32_t nt = n - h - 4 * nb;
-    const uint32_t sa = (uint32_t) (uintptr_t) src;
-    const QH_LDS uint32_t *sw = (const QH_LDS uint32_t *) (src - (sa & 3));
-    const uint32_t s3 = sa & 3;
-    // head and tail: the 4 source bytes at src + i, i = 0 and h + 4 nb
-    const uint32_t it = h + 4 * nb;
-    const uint32_t qt = (s3 + it) >> 2;
-    const uint32_t vh = h ? align_bytes(sw[1], sw[0], s3) : 0u;
-    const uint32_t vt = nt ? align_bytes(sw[qt + 1], sw[qt], (s3 + it) & 3) : 0u;
-    // body: source words from q0, shift r
-    const uint32_t sb = s3 + h, r = sb & 3;
-    const QH_LDS uint32_t *bw = sw + (sb >> 2);
-    QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dstb + h);
-    // Eight dwords per trip, the trip's source words read together and the
-    // last one carried into the next trip (reads past the string stay in
-    // the wave's LDS region or past the allocation, where LDS reads 0).
-    // The first trip's reads go out with the head's and tail's, before any
-    // write (the arena and the stage do not overlap; a wave's LDS operations
-    // run in order, so a read behind a write would wait for it).
-    uint32_t cur = bw[0];
-    uint32_t nw[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        nw[j] = bw[j + 1];
-    write_bytes(dstb, vh, h);
-    write_bytes(dstb + it, vt, nt);
-    for (uint32_t k = 0; k < nb; k += 8)
-    {
-        if (k)
-        {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                nw[j] = bw[k + j + 1];
-        }
-        dw[k] = align_bytes(nw[0], cur, r);
-#pragma unroll
-        for (int j = 1; j < 8; ++j)
-            if (k + j < nb)
-                dw[k + j] = align_bytes(nw[j], nw[j - 1], r);
-        cur = nw[7];
-    }
-}
-
-// The same copy for every lane of the wave at once, with whole dwords and
-// no per-dword lane branches: each lane's body dwords go out in trips of
+// Arena slot -> stage at byte D, for every lane of the wave at once, with
+// whole dwords and no per-dword lane branches (the per-lane copy it replaced,
+// with one lane branch per dword, is neutral-to-slower: profiles/r03_robust): each lane's body dwords go out in trips of
 // eight, the trips and the dwords within them in DESCENDING order, and past
 // its last body dword a lane stores garbage instead of branching.  Lane l's
 // garbage lands only on dwords of later strings (its body starts at D_l <
@@ -675,13 +619,7 @@ struct DecPolicyT
 #ifdef QH_TIME_NO_EMIT                       // timing builds only: no output
         return;
 #endif
-#if QH_COMPACT_WAVE
         compact_wave(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl, sz);
-#else
-        if (sz)
-            compact_string(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl,
-                           sz);
-#endif
     }
 
     // a tile of the batch kernel: base from the look-back
