@@ -46,11 +46,14 @@ qhuff_encode_kernel(EncArgs a)
     __shared__ EncSmem smem;
     QH_LDS EncSmem *sm = (QH_LDS EncSmem *) &smem;
     const int tid = threadIdx.x;
-    enc_tables_load(sm, a.enc, tid);
-    clear_next_launch(a.c);
     Tickets tk;
     tk.init();
-    claim_block_tickets(a.c, tk, &sm->tk, QH_ENC_PER);
+    // the ticket atomics go out first (they queue behind every other
+    // workgroup's on the counters), then the table loads
+    const uint32_t cb = claim_block_issue(a.c, tk, QH_ENC_PER);
+    enc_tables_load(sm, a.enc, tid);
+    claim_block_store(a.c, cb, &sm->tk, QH_ENC_PER);
+    clear_next_launch(a.c);
     __syncthreads();                 // the only workgroup barrier
     EncPolicy pol;
     pol.in = a.in;
