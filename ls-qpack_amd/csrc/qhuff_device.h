@@ -500,6 +500,13 @@ struct LookBack
         return j < 0 ? (kFlagInc | ep(c)) : f;
     }
 
+    // the look-back of tile t (total tot) whose aggregate is published
+    __device__ __forceinline__ void at(uint32_t t, uint32_t tot)
+    {
+        tile = t;
+        s = t / kSuper;
+        total = tot;
+    }
     // publish the aggregate, add to the super accumulator
     __device__ __forceinline__ void start(const Coord &c, uint32_t t,
                                           uint32_t tot)

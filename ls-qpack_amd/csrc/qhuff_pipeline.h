@@ -45,13 +45,21 @@ constexpr int kChunks = 3;                  // 16-byte input chunks per lane
 constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: chunk registers / stages
 
 // A coded tile waiting for its look-back: per-lane output offset and status,
-// the look-back state; its output bytes wait in registers (TileOut).
+// its tile and total; its output bytes wait in registers (TileOut).  (The
+// look-back state -- polls -- lives only for the tile being resolved: kept
+// per pending tile it cost ~14 VGPRs a tile.)
 struct Pending
 {
     bool valid;
     uint32_t excl;                   // this lane's tile-local output offset
     uint32_t stat;                   // this lane's status byte
-    LookBack lb;                     // (its tile and total: lb.tile, lb.total)
+    uint32_t tile, total;            // (wave-uniform)
+    __device__ __forceinline__ LookBack lb() const
+    {
+        LookBack l;
+        l.at(tile, total);
+        return l;
+    }
 };
 
 // Output base of a slow tile (P::slow_tile / slow_tile_at): the batch
@@ -95,15 +103,16 @@ last_tile_end(const Coord &c, uint32_t t, uint64_t end, uint32_t *out_off,
 // resolve a pending tile's base and store it from `o` (every lane)
 template <class P>
 __device__ __forceinline__ void
-flush_tile(const Coord &c, Pending &d, const TileOut<P::kNch> &o, uint8_t *out,
-           uint32_t *out_off, uint8_t *status, uint64_t n, uint32_t it = ~0u)
+flush_tile(const Coord &c, Pending &d, LookBack &lb, const TileOut<P::kNch> &o,
+           uint8_t *out, uint32_t *out_off, uint8_t *status, uint64_t n,
+           uint32_t it = ~0u)
 {
-    const uint64_t base = d.lb.finish(c);
+    const uint64_t base = lb.finish(c);
     prof_stamp(c, it, 7);
 #ifdef QHUFF_PROFILE
-    prof_value(c, it, 8, d.lb.spins_seen);
+    prof_value(c, it, 8, lb.spins_seen);
 #endif
-    const uint32_t tile = d.lb.tile, total = d.lb.total;
+    const uint32_t tile = d.tile, total = d.total;
     o.store(out + base, total);
     const uint32_t lane = lane_id();
     const uint64_t s0 = (uint64_t) tile * P::kTS;
@@ -302,9 +311,9 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     constexpr int D = P::kDepth;
     Pending pend[D];
     TileOut<P::kNch> outs[D];
-    // resolve + store pending tile i (compile-time i)
-    auto flush_at = [&](int i, uint32_t itn) {
-        flush_tile<P>(c, pend[i], outs[i], out, out_off, status, n, itn);
+    // resolve + store pending tile i (compile-time i), polled into lb
+    auto flush_at = [&](int i, LookBack &lb, uint32_t itn) {
+        flush_tile<P>(c, pend[i], lb, outs[i], out, out_off, status, n, itn);
     };
 #pragma unroll
     for (int i = 0; i < D; ++i)
@@ -347,8 +356,12 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         }
         else
             kq4 = tk.claim(c);               // (past the end: never coded)
+        LookBack lbo;                        // the oldest pending tile's
         if (pend[0].valid)
-            pend[0].lb.poll(c);
+        {
+            lbo = pend[0].lb();
+            lbo.poll(c);
+        }
         prof_stamp(c, it, 2);
 
         // codec of t (LDS only when staged)
@@ -368,13 +381,16 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
 
         Pending cur;
         cur.valid = false;
+        LookBack lbc;                        // t's publication
         if (fast)
         {
             // publish t's aggregate, pack t into the LDS out stage
             cur.valid = true;
             cur.excl = excl;
             cur.stat = st;
-            cur.lb.start(c, t, total);
+            cur.tile = t;
+            cur.total = total;
+            lbc.start(c, t, total);
             wave_sync();
             pol.emit(excl, sz, total);
             wave_sync();
@@ -403,9 +419,9 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
         // not at the next iteration's top (look-backs of later super tiles
         // wait on it: encode re-polled the super windows on 1 tile in 3)
         if (cur.valid)
-            cur.lb.super_agg(c);
+            lbc.super_agg(c);
         if (pend[0].valid)
-            flush_at(0, it);
+            flush_at(0, lbo, it);
 #pragma unroll
         for (int i = 0; i + 1 < D; ++i)
         {
@@ -426,8 +442,9 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
             for (int i = 0; i < D; ++i)
                 if (pend[i].valid)
                 {
-                    pend[i].lb.poll(c);
-                    flush_at(i, ~0u);
+                    LookBack l = pend[i].lb();
+                    l.poll(c);
+                    flush_at(i, l, ~0u);
                 }
             pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
                           status, n);
@@ -447,14 +464,18 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     // the drain: every pending tile's polls issued together, then each one
     // resolved and stored (one round trip for all of them, not one each:
     // the last waves' drain ends the kernel)
+    LookBack ld[D];
 #pragma unroll
     for (int i = 0; i < D; ++i)
         if (pend[i].valid)
-            pend[i].lb.poll(c);
+        {
+            ld[i] = pend[i].lb();
+            ld[i].poll(c);
+        }
 #pragma unroll
     for (int i = 0; i < D; ++i)
         if (pend[i].valid)
-            flush_at(i, ~0u);
+            flush_at(i, ld[i], ~0u);
 }
 
 }  // namespace qhuff
