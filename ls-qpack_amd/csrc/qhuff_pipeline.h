@@ -244,30 +244,6 @@ struct NoMid
 // issued, before anything waits for them (the decode kernel stores its
 // window table and joins the workgroup barrier there, so the loads overlap
 // the table's); every wave of the workgroup calls it, tiles or none.
-// (small batches) the tiles a wave claims after its first, each coded by
-// the slow path (out of line: no registers held for it in the pipeline)
-template <class P>
-__device__ __noinline__ void
-small_batch_rest(P pol, Coord c, Tickets tk, const uint8_t *in,
-                 const uint32_t *in_off_p, uint64_t n, uint8_t *out,
-                 uint32_t *out_off, uint8_t *status)
-{
-    const QH_GLB uint32_t *in_off = (const QH_GLB uint32_t *) in_off_p;
-    constexpr uint32_t TS = P::kTS;
-    for (;;)
-    {
-        const uint32_t tt = tk.tile_of(tk.claim(c));
-        if (tt >= c.n_tiles)
-            return;
-        const uint32_t cnt = (uint32_t) min((uint64_t) TS, n - (uint64_t) tt * TS);
-        typename P::Offs o;
-        o.load(in_off, (uint64_t) tt * TS, cnt);
-        Span sp = tile_span(in, o.first(), o.last(), P::kInCap);
-        sp.staged = false;                   // (from global memory)
-        pol.slow_tile(c, tt, cnt, o, sp, 0u, 0u, out, out_off, status, n);
-    }
-}
-
 template <class P, class Mid = NoMid>
 __device__ __forceinline__ void
 tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
@@ -299,10 +275,10 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     // ticket of the third iteration
     typename P::Offs o_cur, o_nxt, o_nn;
     o_cur.load(in_off, (uint64_t) t * TS, cnt_of(t));
-    // small batches (one ticket per wave from the workgroup claim): this
-    // wave's one tile through the pipeline, further ones after the drain
-    const bool small = k1 == kClaimNow;
-    uint32_t tn = small ? 0xffffffffu : tk.tile_of_u(k1);
+    // one ticket per wave from the workgroup claim only when the grid's
+    // waves cover every tile (block_claims_per_wave): this wave's one tile
+    // is then its last, with no claim after it
+    uint32_t tn = k1 == kClaimNow ? 0xffffffffu : tk.tile_of_u(k1);
     o_nxt.load(in_off, (uint64_t) clamp(tn) * TS, cnt_of(clamp(tn)));
     // a wave claims another tile only while its next one is real: a claimed
     // tile is always coded (tickets of a group are handed out in order, so
@@ -509,8 +485,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
     // prologue (~3,000 returning adds there cost a one-round launch ~10 us:
     // 24.3 -> 34.8 us, profiles/r02_k vs r03_u scaling.txt).  Rare: with
     // every workgroup resident the first claim is already past the end.
-    if (small)
-        small_batch_rest(pol, c, tk, in, in_off_p, n, out, out_off, status);
 }
 
 }  // namespace qhuff
