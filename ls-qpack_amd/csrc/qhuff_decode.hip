@@ -67,8 +67,8 @@ qhuff_decode_kernel(DecArgs a)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
     DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
-    uint32_t k0, k1, k2;
-    wave_tickets(tk, &sm->tk, &k0, &k1, &k2);
+    uint32_t t0, k1, k2;
+    wave_tickets(a.c, tk, &sm->tk, &t0, &k1, &k2);
     auto tables = [&]() {
         QH_LDS u32x4 *sw = (QH_LDS u32x4 *) sm->win;
 #pragma unroll
@@ -84,7 +84,7 @@ qhuff_decode_kernel(DecArgs a)
             sm->win[kHoldIdx] = kHoldEntry;
         __syncthreads();             // the tables
     };
-    tile_pipeline(pol, a.c, tk, k0, k1, k2, a.in, a.in_off,
+    tile_pipeline(pol, a.c, tk, t0, k1, k2, a.in, a.in_off,
                   a.n, a.out, a.out_off, a.status, tables);
 }
 

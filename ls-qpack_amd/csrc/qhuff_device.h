@@ -91,6 +91,10 @@ struct Coord
     uint32_t epoch;                         // launch tag carried in flags
     uint32_t n_tiles;
     uint32_t cap_super;                     // sacc entries per parity
+    uint32_t spread;                        // > 0: the first `spread` waves of
+                                            // each workgroup take one tile
+                                            // each from counter 0 (batches
+                                            // the grid covers; qhuff_pipeline.h)
 };
 
 struct Coord;

@@ -59,11 +59,11 @@ qhuff_encode_kernel(EncArgs a)
     pol.in = a.in;
     pol.mode = a.mode;
     pol.sm = sm;
-    pol.wv = &sm->w[tid >> 6];
+    pol.wv = &sm->w[__builtin_amdgcn_readfirstlane(tid >> 6)];
     pol.dense = false;
-    uint32_t k0, k1, k2;
-    wave_tickets(tk, &sm->tk, &k0, &k1, &k2);
-    tile_pipeline(pol, a.c, tk, k0, k1, k2, a.in, a.in_off,
+    uint32_t t0, k1, k2;
+    wave_tickets(a.c, tk, &sm->tk, &t0, &k1, &k2);
+    tile_pipeline(pol, a.c, tk, t0, k1, k2, a.in, a.in_off,
                   a.n, a.out, a.out_off, nullptr);
 }
 

@@ -141,6 +141,8 @@ struct qhuff_ctx
     int device;
     int n_cu;
     uint32_t enc_grid, dec_grid;         // workgroups per launch
+    bool spread;                         // spread batches the grid covers
+                                         // (grid_for; QHUFF_NO_SPREAD=1: off)
     uint32_t hash_grid;                  // resident hash workgroups
     hipStream_t own_stream;
     DevTables *tab;                      // device
@@ -290,6 +292,8 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     }
     c->epoch = 0;
     {
+        const char *ns = getenv("QHUFF_NO_SPREAD");
+        c->spread = !(ns && *ns && *ns != '0');
         // tuning override: fewer workgroups per CU than fit
         const char *g = getenv("QHUFF_GRID_WG_PER_CU");
         if (g)
@@ -511,17 +515,29 @@ coord(qhuff_ctx *c, uint64_t tiles)
     k.err_host = c->err_host_dev;
     k.epoch = c->epoch;
     k.n_tiles = (uint32_t) tiles;
+    k.spread = 0;
     return k;
 }
 
-// Workgroups for a launch of `tiles` tiles: tiles are claimed from tickets
-// (any grid size is correct); ticket groups are blockIdx % 8, so a grid of
-// more than 8 blocks is a multiple of 8 (balanced groups), at most `cap`
-// (the co-resident count: more would only queue).
+// Workgroups for a launch of `tiles` tiles, at most `cap` (the co-resident
+// count: more would only queue); tiles are claimed from tickets, so any grid
+// size is correct.  A batch of at most one tile per wave of the full grid
+// is spread: one workgroup per tile up to `cap`, the first *spread waves
+// of each taking one tile each (Coord::spread; fewer waves per CU code
+// their tile faster, and the whole batch is handed out by one returning
+// add per workgroup on one counter, in order).  Larger batches: every wave,
+// ticket groups.
 static uint32_t
-grid_for(uint64_t tiles, uint64_t waves_per_block, uint32_t cap)
+grid_for(const qhuff_ctx *c, uint64_t tiles, uint64_t waves_per_block,
+         uint32_t cap, uint32_t *spread)
 {
-    // (any number of workgroups: each covers every ticket group)
+    *spread = 0;
+    if (c->spread && tiles <= (uint64_t) cap * waves_per_block)
+    {
+        const uint32_t g = (uint32_t) (tiles < cap ? tiles : cap);
+        *spread = (uint32_t) ((tiles + g - 1) / g);
+        return g;
+    }
     const uint64_t need = (tiles + waves_per_block - 1) / waves_per_block;
     return (uint32_t) (need < cap ? need : cap);
 }
@@ -556,7 +572,7 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.mode = mode;
     a.c = coord(c, tiles);
     const uint64_t wpb = (uint64_t) encode_waves_per_block();
-    const uint32_t grid = grid_for(tiles, wpb, c->enc_grid);
+    const uint32_t grid = grid_for(c, tiles, wpb, c->enc_grid, &a.c.spread);
     HIPCHK(c, launch_encode(a, grid, st));
     return finish_launch(c, st);
 }
@@ -592,7 +608,7 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.c = coord(c, tiles);
     a.lp = c->lp;
     const uint64_t wpb = (uint64_t) decode_waves_per_block();
-    const uint32_t grid = grid_for(tiles, wpb, c->dec_grid);
+    const uint32_t grid = grid_for(c, tiles, wpb, c->dec_grid, &a.c.spread);
     HIPCHK(c, launch_decode(a, grid, st));
     return finish_launch(c, st);
 }

@@ -154,7 +154,11 @@ wait_vm_all()
 // whichever workgroup claimed it would need the whole grid resident: with
 // only some workgroups resident, e.g. beside another context, a group's
 // tickets could run ahead of another's and the look-backs above the gap
-// wait for tiles no running wave can claim).
+// wait for tiles no running wave can claim).  Spread launches
+// (Coord::spread > 0, batches of at most one tile per wave of the grid,
+// qhuff_host.cpp grid_for): workgroup b's thread 0 adds `spread` to
+// counter 0 alone and its first `spread` waves take those tiles, one each;
+// the claimed tiles are always a prefix, so the same holds.
 constexpr uint32_t kClaimNow = 0xffffffffu;   // ticket: claim it in the wave
                                               // (tile_pipeline)
 struct BlockTickets
@@ -189,7 +193,15 @@ claim_block_issue(const Coord &c, const Tickets &tk, uint32_t maxper)
 {
     const uint32_t t = threadIdx.x;
     uint32_t b = 0;
-    if (t < kTickGroups)
+    if (c.spread)
+    {
+        // one counter, `spread` consecutive tiles per workgroup
+        if (t == 0)
+            b = __hip_atomic_fetch_add(tk.counter(c, 0), c.spread,
+                                       __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    }
+    else if (t < kTickGroups)
     {
         const uint32_t nq = tick_group_waves(t);
         if (nq)
@@ -209,7 +221,7 @@ claim_block_store(const Coord &c, uint32_t b, QH_LDS BlockTickets *bt,
     if (t < kTickGroups)
         bt->base[t] = b;
     if (t == 0)
-        bt->per = block_claims_per_wave(c, maxper);
+        bt->per = c.spread ? 1u : block_claims_per_wave(c, maxper);
 }
 
 __device__ __forceinline__ void
@@ -219,17 +231,25 @@ claim_block_tickets(const Coord &c, const Tickets &tk, QH_LDS BlockTickets *bt,
     claim_block_store(c, claim_block_issue(c, tk, maxper), bt, maxper);
 }
 
-// this wave's first tickets (after the workgroup barrier)
+// this wave's first tile t0 and its next tickets (after the workgroup
+// barrier)
 __device__ __forceinline__ void
-wave_tickets(const Tickets &tk, const QH_LDS BlockTickets *bt, uint32_t *k0,
-             uint32_t *k1, uint32_t *k2)
+wave_tickets(const Coord &c, const Tickets &tk, const QH_LDS BlockTickets *bt,
+             uint32_t *t0, uint32_t *k1, uint32_t *k2)
 {
+    if (c.spread)
+    {
+        const uint32_t w = threadIdx.x >> 6;
+        *t0 = w < c.spread ? bt->base[0] + w : 0xffffffffu;
+        *k1 = *k2 = kClaimNow;
+        return;
+    }
     // rank among this workgroup's waves of the same group (waves w and
     // w + kTickGroups share one)
     const uint32_t r = (threadIdx.x >> 6) / kTickGroups;
     const uint32_t nq = tick_group_waves(tk.g);
     const uint32_t per = bt->per;
-    *k0 = bt->base[tk.g] + r;
+    *t0 = tk.tile_of_u(bt->base[tk.g] + r);
     *k1 = per >= 2 ? bt->base[tk.g] + nq + r : kClaimNow;
     *k2 = per >= 3 ? bt->base[tk.g] + 2 * nq + r : kClaimNow;
 }
@@ -246,16 +266,16 @@ struct NoMid
 // the table's); every wave of the workgroup calls it, tiles or none.
 template <class P, class Mid = NoMid>
 __device__ __forceinline__ void
-tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t k0,
+tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
               uint32_t k1, uint32_t k2, const uint8_t *in,
               const uint32_t *in_off_p, uint64_t n, uint8_t *out,
               uint32_t *out_off, uint8_t *status, Mid mid = Mid())
 {
     const QH_GLB uint32_t *in_off = (const QH_GLB uint32_t *) in_off_p;
     const uint32_t nt = c.n_tiles;
-    // tiles of this wave's first iterations (tickets k0 < k1 < k2 claimed
-    // for the whole block in the kernel prologue, or kClaimNow)
-    uint32_t t = tk.tile_of_u(k0);
+    // this wave's first tile t0 and the tickets k1 < k2 of its next ones
+    // (claimed for the whole block in the kernel prologue, or kClaimNow)
+    uint32_t t = t0;
     if (t >= nt)
     {
         mid();
