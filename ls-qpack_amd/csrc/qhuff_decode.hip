@@ -66,7 +66,7 @@ qhuff_decode_kernel(DecArgs a)
     // __syncthreads() would drain them)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
-    DecPolicy pol{a.in, sm, &sm->w[tid >> 6], 0};
+    DecPolicy pol{a.in, sm, &sm->w[__builtin_amdgcn_readfirstlane(tid >> 6)], 0};
     uint32_t t0, k1, k2;
     wave_tickets(a.c, tk, &sm->tk, &t0, &k1, &k2);
     auto tables = [&]() {
