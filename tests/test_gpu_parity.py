@@ -274,6 +274,51 @@ def test_edge_batches(codec):
     check_decode(codec, h, ho)
 
 
+def _launch_shape_check(c, n, seed):
+    import qhuff
+    data, off = qhuff.synth_batch(n, seed=seed)
+    g_out, g_off = check_encode(c, data, off, 0)
+    out, oo, st = check_decode(c, g_out, g_off)
+    assert not st.any()
+    assert np.array_equal(out, data) and np.array_equal(oo, off)
+
+
+def test_launch_shapes(codec):
+    """Batch sizes around the launch-shape boundaries (qhuff_host.cpp
+    grid_for): spread launches (one tile per wave, one workgroup per tile up
+    to the grid: 1..W tiles) and ticket-group launches with one, two and
+    three prologue tickets per wave (W = the resident grid's waves)."""
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    W = n_cu * 12
+    tiles = sorted({1, 7, 8, 9, n_cu - 1, n_cu, n_cu + 1, 4 * n_cu + 3,
+                    W - 1, W, W + 1, 2 * W, 2 * W + 1, 3 * W, 3 * W + 1})
+    for i, t in enumerate(tiles):
+        for n in (64 * t, 64 * t - 37):
+            if n > 0:
+                _launch_shape_check(codec, n, seed=100 + 2 * i + (n % 2))
+
+
+def test_launch_shapes_no_spread():
+    """QHUFF_NO_SPREAD=1 (read when a context is created): batches the grid
+    covers fill whole workgroups instead; same results."""
+    import qhuff
+    old = os.environ.get("QHUFF_NO_SPREAD")
+    os.environ["QHUFF_NO_SPREAD"] = "1"
+    try:
+        c = qhuff.Codec(0)
+    finally:
+        if old is None:
+            del os.environ["QHUFF_NO_SPREAD"]
+        else:
+            os.environ["QHUFF_NO_SPREAD"] = old
+    try:
+        n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+        for t in (1, 9, n_cu + 1, n_cu * 12):
+            _launch_shape_check(c, 64 * t - 5, seed=7 + t)
+    finally:
+        c.close()
+
+
 def test_full_size_round_trip(codec):
     """BASELINE config 2/3 size (1M strings, U[8,64] token alphabet): GPU
     sizes and bytes equal the oracle's; decode(encode(x)) == x."""
