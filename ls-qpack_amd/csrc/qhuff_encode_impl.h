@@ -10,9 +10,13 @@
 // us); the oldest parked in LDS instead still spilled 5 VGPRs in the dense
 // pass (72.8 vs 65.5 us, profiles/r02_h); round 3, with the pending state
 // slimmed and the next tile's loads issued after the dense pass, 2 VGPRs
-// still spill: 68.3 vs 63.0 us (profiles/r03_i)
+// still spill: 68.3 vs 63.0 us (profiles/r03_i).  Then, with the wave
+// pointer and the flushed tile wave-uniform (readfirstlane) and the
+// flush's per-lane addresses rebuilt per flush instead of held, depth 3
+// fits in 168 VGPRs with no spill: encode 0.964 of depth 2 (four pairs),
+// look-back re-polls 0.83 -> 0.18 per tile (profiles/r03_e3)
 #ifndef QH_ENC_DEPTH
-#define QH_ENC_DEPTH 2
+#define QH_ENC_DEPTH 3
 #endif
 
 namespace qhuff {

@@ -112,9 +112,15 @@ flush_tile(const Coord &c, Pending &d, LookBack &lb, const TileOut<P::kNch> &o,
 #ifdef QHUFF_PROFILE
     prof_value(c, it, 8, lb.spins_seen);
 #endif
-    const uint32_t tile = d.tile, total = d.total;
+    // (wave-uniform: readfirstlane lets the offsets / status addresses
+    // live in SGPRs)
+    const uint32_t tile = __builtin_amdgcn_readfirstlane(d.tile);
+    const uint32_t total = d.total;
     o.store(out + base, total);
-    const uint32_t lane = lane_id();
+    uint32_t lane = lane_id();
+    // (opaque: the per-lane addresses are rebuilt here, not hoisted out of
+    // the tile loop as a register pair each)
+    asm volatile("" : "+v"(lane));
     const uint64_t s0 = (uint64_t) tile * P::kTS;
     const uint32_t cnt = (uint32_t) min((uint64_t) P::kTS, n - s0);
     if (lane < cnt)
