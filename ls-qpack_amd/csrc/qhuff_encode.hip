@@ -31,9 +31,11 @@
 // (global reads / per-lane global writes).
 #include "qhuff_encode_impl.h"
 
-// tickets claimed per wave in the prologue, at most (tile_pipeline)
+// tickets claimed per wave in the prologue, at most (tile_pipeline); 3
+// since the encode runs three pending tiles (0.971 of 2 + the late third
+// ticket, four pairs: profiles/r03_ep3)
 #ifndef QH_ENC_PER
-#define QH_ENC_PER 2
+#define QH_ENC_PER 3
 #endif
 
 namespace qhuff {
