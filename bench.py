@@ -47,10 +47,6 @@ def parse():
     ap.add_argument("--n", type=int, default=1 << 20,
                     help="strings per GPU (default 1M)")
     ap.add_argument("--copies", type=int, default=4)
-    ap.add_argument("--event-every", type=int, default=4,
-                    help="bracket the kernels of every E-th timed step with "
-                         "HIP timing events (each timing event costs ~3.6 us "
-                         "of queue time on MI355X; tools/overlap_probe.py)")
     ap.add_argument("--alphabet", default="token", choices=["token", "base64"])
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="wall seconds per CPU-baseline leg (0 = skip)")
@@ -67,6 +63,11 @@ def parse():
                     default=True,
                     help="also time the PCIe-inclusive host-memory path "
                          "(rank 0; never `value`)")
+    ap.add_argument("--workloads", action=argparse.BooleanOptionalAction,
+                    default=True,
+                    help="also time the real-workload batches (QIF corpora, "
+                         "base64, long-code alphabet C; rank 0; never "
+                         "`value`)")
     ap.add_argument("--probe-launch", action="store_true",
                     help=argparse.SUPPRESS)   # tests: ranks meet, no GPU
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
@@ -266,18 +267,12 @@ def main():
 
     stream = torch.cuda.current_stream()
 
-    def step(i, ev=None):
+    def step(i):
         k = i % args.copies
         j = (i + args.copies // 2) % args.copies
-        if ev:
-            ev[0].record(stream)
         codec.encode_into(d_in[k], d_off[k], n, 0, e_out[k], e_off[k], stream)
-        if ev:
-            ev[1].record(stream)
         codec.decode_into(d_hin[j], d_hoff[j], n, d_out[j], d_ooff[j],
                           d_st[j], stream)
-        if ev:
-            ev[2].record(stream)
 
     for i in range(args.warmup):
         step(i)
@@ -291,29 +286,30 @@ def main():
               and bool((d_st[0] == 0).all())
               and torch.equal(d_ooff[0], d_off[0]))
 
-    # kernel durations for the roofline: HIP events around the kernels of
-    # every E-th timed step (the last of each group of E, so never the first
-    # step after the barrier; the only step when K < E); the rest run
-    # without events
-    ev_every = max(1, min(args.event_every, args.steps))
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
-           if i % ev_every == ev_every - 1 else None
-           for i in range(args.steps)]
-    ev_used = [e for e in evs if e]
+    # kernel durations for the roofline: every launch of the timed region
+    # carries a HIP event pair stamped by its own dispatch (qhuff_timing_*:
+    # hipExtLaunchKernel's start / stop events -- the kernel's device time,
+    # as rocprofv3's kernel trace measures it, and no timing packets between
+    # the launches); the last QHUFF_TIMING_SLOTS launches are read back
+    codec.timing(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i, evs[i])
+        step(args.warmup + i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     wall = t1 - t0
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev_used) / len(ev_used)
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev_used) / len(ev_used)
+    timed = codec.timing_read()
+    codec.timing(False)
+    enc_t = [u for k, u in timed if k == qhuff.KIND_ENCODE]
+    dec_t = [u for k, u in timed if k == qhuff.KIND_DECODE]
+    enc_ms = sum(enc_t) / len(enc_t) * 1e-3
+    dec_ms = sum(dec_t) / len(dec_t) * 1e-3
     # the kernels' sticky error word (look-back spin / offset range): a
     # launch that raised one produced no valid output
     dev_err = codec.device_error()
@@ -354,7 +350,11 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": kname, "kernel_us": round(kms * 1e3, 2),
             "alg_bytes": alg,
-            "event_steps": "%d of %d timed steps" % (len(ev_used), args.steps)}
+            "timing": "mean over %d %s launches of the timed region, each "
+                      "dispatched with HIP start/stop events stamped by the "
+                      "dispatch itself (hipExtLaunchKernel)"
+                      % (len(dec_t if kname == "qhuff_decode_kernel" else enc_t),
+                         kname)}
     if pmc_src:
         roof["traffic_source"] = pmc_src
 
@@ -368,26 +368,24 @@ def main():
     hh = n // 2
     h1 = torch.empty(hh, dtype=torch.int32, device=dev)
     h2 = torch.empty(hh, dtype=torch.int32, device=dev)
-    # per launch, the way enc/dec are timed: one event pair around each
-    # launch on the launch stream (a pair around back-to-back launches would
-    # count the gaps between them)
+    # timed the way enc/dec are: each launch's own dispatch timestamps
     for i in range(3):
         codec.xxh32_headers_into(d_in[i % args.copies], d_off[i % args.copies],
                                  hh, qhuff.XXH_SEED, h1, h2, stream)
-    hev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)]
-           for _ in range(max(1, min(args.steps, 20)))]
-    for i, (e0, e1) in enumerate(hev):
-        e0.record(stream)
+    codec.timing(True)
+    nh = max(1, min(args.steps, 20))
+    for i in range(nh):
         codec.xxh32_headers_into(d_in[i % args.copies], d_off[i % args.copies],
                                  hh, qhuff.XXH_SEED, h1, h2, stream)
-        e1.record(stream)
-    torch.cuda.synchronize()
-    hash_ms = sum(e0.elapsed_time(e1) for e0, e1 in hev) / len(hev)
+    ht = [u for k, u in codec.timing_read() if k == qhuff.KIND_HASH]
+    codec.timing(False)
+    hash_ms = sum(ht) / len(ht) * 1e-3
     hash_bytes = int(off[2 * hh])
     hash_alg = hash_bytes + 4 * (2 * hh + 1) + 8 * hh
     hashing = {"kernel": "qhuff_hash_kernel", "headers": hh,
                "kernel_us": round(hash_ms * 1e3, 2),
-               "timing": "HIP events around each of %d launches" % len(hev),
+               "timing": "mean over %d launches, dispatch-stamped HIP "
+                         "events (hipExtLaunchKernel)" % len(ht),
                "payload_gbps": round(hash_bytes / (hash_ms * 1e-3) / 1e9, 2),
                "alg_bytes": hash_alg,
                "roofline_frac": round(hash_alg / (hash_ms * 1e-3) / 1e9
@@ -401,6 +399,11 @@ def main():
                 hashing["traffic"] = ent.get("hbm_bytes_per_launch")
         except Exception:
             pass
+
+    work = None
+    if args.workloads and rank == 0 and world == 1:
+        work = run_workloads(args, np, torch, qhuff, codec, dev, stream, n,
+                             raw_bytes, enc_ms, dec_ms)
 
     host = None
     if args.host_path and rank == 0:
@@ -457,6 +460,8 @@ def main():
         }
         if host:
             line["host_path"] = host
+        if work:
+            line["workloads"] = work
         print(json.dumps(line), flush=True)
     codec.close()
     if world > 1:
@@ -501,6 +506,73 @@ def cpu_baseline(args, data, off, h_np, h_off_np, n, raw_bytes):
                        "at every usable CPU" % (n, args.cpu_seconds)),
             "threads_1": legs["threads_1"], "threads_all": legs["threads_all"],
             "host": cpus, "cpu_model": cpu_model()}
+
+
+def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
+                  enc_ms_syn, dec_ms_syn):
+    """Real-workload shapes, never `value`: 1M-string
+    batches of the reference's QIF corpora (names and values in wire order,
+    repeated), of the base64 alphabet and of the long-code alphabet C; each
+    encoded and decoded K times with dispatch-stamped timing (kernel device
+    time), the round trip checked, and the tile-path shares of each batch
+    (qhuff/workload.py: slow tiles, variable arena slots, encode fallback)."""
+    from qhuff import workload as W
+    K = 10
+    data_dir = os.path.join(ROOT, "tests", "golden", "data")
+    batches = [
+        ("qif_corpus", "tests/golden/data/{fb-req,fb-resp,long-codes,netbsd}"
+                       ".qif names and values in wire order, repeated",
+         W.corpus_batch(n, data_dir)),
+        ("base64", "synthetic U[8,64], base64 alphabet",
+         qhuff.synth_batch(n, alphabet=qhuff.BASE64_ALPHABET)),
+        ("alphabet_c", "synthetic U[8,64], token alphabet + ~2 % long-code "
+                       "bytes {1,2,6,92,141}", W.alphabet_c(n)),
+    ]
+    syn_gbps = 2 * raw_syn / ((enc_ms_syn + dec_ms_syn) * 1e-3) / 1e9
+    out = {"strings": n, "launches_per_kernel": K,
+           "synthetic_token_gbps": round(syn_gbps, 1)}
+    for name, desc, (data, off) in batches:
+        raw = int(off[-1])
+        d = torch.from_numpy(data).to(dev)
+        o = torch.from_numpy(off.view(np.int32)).to(dev)
+        ecap = qhuff.encode_bound(raw, n, 0)
+        eo = torch.empty(ecap, dtype=torch.uint8, device=dev)
+        eoo = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        codec.encode_into(d, o, n, 0, eo, eoo, stream)
+        torch.cuda.synchronize()
+        hoff = eoo.cpu().numpy().view(np.uint32).copy()
+        hb = int(hoff[-1])
+        h = eo[:hb].clone()
+        do = torch.empty(qhuff.decode_bound(hb, n), dtype=torch.uint8,
+                         device=dev)
+        doo = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        codec.decode_into(h, eoo, n, do, doo, st, stream)
+        torch.cuda.synchronize()
+        codec.timing(True)
+        for _ in range(K):
+            codec.encode_into(d, o, n, 0, eo, eoo, stream)
+        for _ in range(K):
+            codec.decode_into(h, eoo, n, do, doo, st, stream)
+        tm = codec.timing_read()
+        codec.timing(False)
+        eu = [u for k, u in tm if k == qhuff.KIND_ENCODE]
+        du = [u for k, u in tm if k == qhuff.KIND_DECODE]
+        e_us, d_us = sum(eu) / len(eu), sum(du) / len(du)
+        ok = (torch.equal(do[:raw], d) and not bool(st.any())
+              and np.array_equal(doo.cpu().numpy().view(np.uint32), off))
+        gbps = 2 * raw / ((e_us + d_us) * 1e-6) / 1e9
+        ent = {"data": desc, "raw_bytes": raw, "huff_bytes": hb,
+               "enc_kernel_us": round(e_us, 2), "dec_kernel_us": round(d_us, 2),
+               "enc_payload_gbps": round(raw / (e_us * 1e-6) / 1e9, 1),
+               "dec_payload_gbps": round(raw / (d_us * 1e-6) / 1e9, 1),
+               "enc_dec_gbps": round(gbps, 1),
+               "vs_synthetic_token": round(gbps / syn_gbps, 3),
+               "roundtrip_ok": bool(ok)}
+        ent.update(W.tile_shares(data, off, hoff))
+        out[name] = ent
+        del d, o, eo, eoo, h, do, doo, st
+    return out
 
 
 def run_config4(args, np, torch, qhuff):

@@ -36,9 +36,18 @@
 extern "C" {
 #endif
 
-/* 2: qhuff_huff_decode_ex (the reference's full argument list) added beside
- * the 5-argument qhuff_huff_decode of version 1, which is unchanged */
-#define QHUFF_ABI_VERSION 3
+/* ABI versions:
+ *   1  batch encode / decode, host path, per-string mirrors.  (An early
+ *      header of this version declared qhuff_huff_decode with 7 arguments,
+ *      state and final included; the symbol takes 5 -- a caller built
+ *      against that header links but its state / final are ignored: use
+ *      qhuff_huff_decode_ex and check qhuff_abi_version() >= 2.)
+ *   2  qhuff_huff_decode_ex (the reference's full argument list) beside the
+ *      5-argument qhuff_huff_decode, which is unchanged
+ *   3  the low-latency service (qhuff_svc_*) and, in qhuff_lsqpack.h,
+ *      qhuff_lsqpack_set_context
+ *   4  launch timing (qhuff_timing_enable / qhuff_timing_read) */
+#define QHUFF_ABI_VERSION 4
 
 /* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
 int qhuff_abi_version(void);
@@ -346,6 +355,23 @@ int qhuff_device_error(qhuff_ctx *ctx);
  * max_words per-wave phase stamps of the last launch into dst and return
  * the number available; 0 in normal builds.  Synchronous. */
 uint64_t qhuff_profile_read(qhuff_ctx *ctx, uint64_t *dst, uint64_t max_words);
+
+/* Launch timing.  With timing on, every encode / decode / hash launch of
+ * the context is dispatched with a pair of HIP events that carry the
+ * dispatch's own start and end timestamps (hipExtLaunchKernel: the kernel's
+ * device time, what rocprofv3's kernel trace reports, with no timing
+ * packets queued around the launch), kept in a ring of the last
+ * QHUFF_TIMING_SLOTS launches.  qhuff_timing_read waits for them and
+ * returns, oldest first, the launches timed since timing was enabled or
+ * last read (at most `max`, the most recent ones): kind[i] (QHUFF_KIND_*)
+ * and us[i], microseconds.  qhuff_timing_enable(ctx, 0) turns it off.
+ * Return QHUFF_OK / the count, or QHUFF_E*. */
+#define QHUFF_TIMING_SLOTS 256
+#define QHUFF_KIND_ENCODE 0
+#define QHUFF_KIND_DECODE 1
+#define QHUFF_KIND_HASH   2
+int qhuff_timing_enable(qhuff_ctx *ctx, int on);
+int qhuff_timing_read(qhuff_ctx *ctx, uint32_t *kind, double *us, uint32_t max);
 
 /* ---- multi-GPU sharding helpers (host arithmetic only) ----------------
  * Byte-balanced contiguous partition of a batch into g shards: writes

@@ -25,6 +25,8 @@
 // the look-back has resolved the tile's output base.
 #include "qhuff_decode_impl.h"
 
+#include <hip/hip_ext.h>
+
 // tickets claimed per wave in the prologue, at most (tile_pipeline)
 #ifndef QH_DEC_PER
 #define QH_DEC_PER 3
@@ -89,10 +91,15 @@ qhuff_decode_kernel(DecArgs a)
 }
 
 hipError_t
-launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st)
+launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st, hipEvent_t ev0,
+              hipEvent_t ev1)
 {
-    hipLaunchKernelGGL(qhuff_decode_kernel, dim3(grid), dim3(64 * kWaves),
-                       0, st, a);
+    if (ev0)
+        hipExtLaunchKernelGGL(qhuff_decode_kernel, dim3(grid), dim3(64 * kWaves), 0, st,
+                              ev0, ev1, 0, a);
+    else
+        hipLaunchKernelGGL(qhuff_decode_kernel, dim3(grid), dim3(64 * kWaves),
+                           0, st, a);
     return hipGetLastError();
 }
 

@@ -31,6 +31,8 @@
 // (global reads / per-lane global writes).
 #include "qhuff_encode_impl.h"
 
+#include <hip/hip_ext.h>
+
 // tickets claimed per wave in the prologue, at most (tile_pipeline); 3
 // since the encode runs three pending tiles (0.971 of 2 + the late third
 // ticket, four pairs: profiles/r03_ep3)
@@ -70,10 +72,15 @@ qhuff_encode_kernel(EncArgs a)
 }
 
 hipError_t
-launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st)
+launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st, hipEvent_t ev0,
+              hipEvent_t ev1)
 {
-    hipLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(64 * kWaves),
-                       0, st, a);
+    if (ev0)
+        hipExtLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(64 * kWaves), 0, st,
+                              ev0, ev1, 0, a);
+    else
+        hipLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(64 * kWaves),
+                           0, st, a);
     return hipGetLastError();
 }
 

@@ -22,6 +22,8 @@
 // costs its name + value bytes + 8 B of offsets + 8 B of hashes.
 #include "qhuff_kernels.h"
 
+#include <hip/hip_ext.h>
+
 namespace qhuff {
 
 constexpr int kHashWaves = 8;                      // waves per workgroup
@@ -253,14 +255,25 @@ qhuff_hash_kernel(HashArgs a)
 }
 
 hipError_t
-launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st)
+launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st,
+            hipEvent_t ev0, hipEvent_t ev1)
 {
     const uint64_t tiles = (a.n + kWT - 1) / kWT;
     const uint64_t need = (tiles + kHashWaves - 1) / kHashWaves;
     const uint32_t grid = (uint32_t) (need < max_grid ? need : max_grid);
-    hipLaunchKernelGGL(qhuff_hash_kernel, dim3(grid), dim3(64 * kHashWaves),
-                       0, st, a);
+    if (ev0)
+        hipExtLaunchKernelGGL(qhuff_hash_kernel, dim3(grid),
+                              dim3(64 * kHashWaves), 0, st, ev0, ev1, 0, a);
+    else
+        hipLaunchKernelGGL(qhuff_hash_kernel, dim3(grid), dim3(64 * kHashWaves),
+                           0, st, a);
     return hipGetLastError();
+}
+
+int
+hash_waves_per_block()
+{
+    return kHashWaves;
 }
 
 hipError_t

@@ -141,8 +141,6 @@ struct qhuff_ctx
     int device;
     int n_cu;
     uint32_t enc_grid, dec_grid;         // workgroups per launch
-    bool spread;                         // spread batches the grid covers
-                                         // (grid_for; QHUFF_NO_SPREAD=1: off)
     uint32_t hash_grid;                  // resident hash workgroups
     hipStream_t own_stream;
     DevTables *tab;                      // device
@@ -181,6 +179,12 @@ struct qhuff_ctx
     // the low-latency service attached by qhuff_svc_open (small host-path
     // calls on this context go through it)
     qhuff_svc *svc;
+    // launch timing (qhuff_timing_enable): a start / stop event pair per
+    // launch, a ring of the last QHUFF_TIMING_SLOTS launches
+    hipEvent_t *tev;                     // [2 * QHUFF_TIMING_SLOTS], or null
+    bool t_on;
+    uint64_t t_next, t_first;            // launches timed / first unread
+    uint8_t t_kind[QHUFF_TIMING_SLOTS];
     char err_msg[256];
 };
 
@@ -292,8 +296,6 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     }
     c->epoch = 0;
     {
-        const char *ns = getenv("QHUFF_NO_SPREAD");
-        c->spread = !(ns && *ns && *ns != '0');
         // tuning override: fewer workgroups per CU than fit
         const char *g = getenv("QHUFF_GRID_WG_PER_CU");
         if (g)
@@ -344,6 +346,12 @@ qhuff_close(qhuff_ctx *c)
         (void) hipHostFree(c->h_stage);
     if (c->prof)
         (void) hipFree(c->prof);
+    if (c->tev)
+    {
+        for (unsigned i = 0; i < 2 * QHUFF_TIMING_SLOTS; ++i)
+            (void) hipEventDestroy(c->tev[i]);
+        delete[] c->tev;
+    }
     if (c->own_stream)
         (void) hipStreamDestroy(c->own_stream);
     if (c->ev_last)
@@ -519,6 +527,78 @@ coord(qhuff_ctx *c, uint64_t tiles)
     return k;
 }
 
+// the event pair of the next launch (kind QHUFF_KIND_*) with timing on:
+// *e0 = *e1 = null otherwise
+static void
+timing_slot(qhuff_ctx *c, uint32_t kind, hipEvent_t *e0, hipEvent_t *e1)
+{
+    *e0 = *e1 = nullptr;
+    if (!c->t_on)
+        return;
+    const uint32_t k = (uint32_t) (c->t_next % QHUFF_TIMING_SLOTS);
+    c->t_kind[k] = (uint8_t) kind;
+    ++c->t_next;
+    *e0 = c->tev[2 * k];
+    *e1 = c->tev[2 * k + 1];
+}
+
+extern "C" int
+qhuff_timing_enable(qhuff_ctx *c, int on)
+{
+    if (!c)
+        return QHUFF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (on && !c->tev)
+    {
+        hipEvent_t *ev = new (std::nothrow) hipEvent_t[2 * QHUFF_TIMING_SLOTS]();
+        if (!ev)
+            return QHUFF_ENOMEM;
+        for (unsigned i = 0; i < 2 * QHUFF_TIMING_SLOTS; ++i)
+        {
+            const hipError_t e = hipEventCreate(&ev[i]);
+            if (e != hipSuccess)
+            {
+                for (unsigned j = 0; j < i; ++j)
+                    (void) hipEventDestroy(ev[j]);
+                delete[] ev;
+                return fail(c, e, "hipEventCreate (timing)");
+            }
+        }
+        c->tev = ev;
+    }
+    c->t_on = on != 0;
+    c->t_first = c->t_next;
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_timing_read(qhuff_ctx *c, uint32_t *kind, double *us, uint32_t max)
+{
+    if (!c || (max && (!kind || !us)))
+        return QHUFF_EINVAL;
+    if (!c->tev)
+        return 0;
+    HIPCHK(c, hipSetDevice(c->device));
+    uint64_t a = c->t_first;
+    const uint64_t b = c->t_next;
+    if (b - a > QHUFF_TIMING_SLOTS)
+        a = b - QHUFF_TIMING_SLOTS;
+    if (b - a > max)
+        a = b - max;
+    uint32_t n = 0;
+    for (uint64_t i = a; i < b; ++i, ++n)
+    {
+        const uint32_t k = (uint32_t) (i % QHUFF_TIMING_SLOTS);
+        HIPCHK(c, hipEventSynchronize(c->tev[2 * k + 1]));
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->tev[2 * k], c->tev[2 * k + 1]));
+        kind[n] = c->t_kind[k];
+        us[n] = 1e3 * (double) ms;
+    }
+    c->t_first = b;
+    return (int) n;
+}
+
 // Workgroups for a launch of `tiles` tiles, at most `cap` (the co-resident
 // count: more would only queue); tiles are claimed from tickets, so any grid
 // size is correct.  A batch of at most one tile per wave of the full grid
@@ -531,8 +611,9 @@ static uint32_t
 grid_for(const qhuff_ctx *c, uint64_t tiles, uint64_t waves_per_block,
          uint32_t cap, uint32_t *spread)
 {
+    (void) c;
     *spread = 0;
-    if (c->spread && tiles <= (uint64_t) cap * waves_per_block)
+    if (tiles <= (uint64_t) cap * waves_per_block)
     {
         const uint32_t g = (uint32_t) (tiles < cap ? tiles : cap);
         *spread = (uint32_t) ((tiles + g - 1) / g);
@@ -573,7 +654,9 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.c = coord(c, tiles);
     const uint64_t wpb = (uint64_t) encode_waves_per_block();
     const uint32_t grid = grid_for(c, tiles, wpb, c->enc_grid, &a.c.spread);
-    HIPCHK(c, launch_encode(a, grid, st));
+    hipEvent_t e0, e1;
+    timing_slot(c, QHUFF_KIND_ENCODE, &e0, &e1);
+    HIPCHK(c, launch_encode(a, grid, st, e0, e1));
     return finish_launch(c, st);
 }
 
@@ -609,7 +692,9 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.lp = c->lp;
     const uint64_t wpb = (uint64_t) decode_waves_per_block();
     const uint32_t grid = grid_for(c, tiles, wpb, c->dec_grid, &a.c.spread);
-    HIPCHK(c, launch_decode(a, grid, st));
+    hipEvent_t e0, e1;
+    timing_slot(c, QHUFF_KIND_DECODE, &e0, &e1);
+    HIPCHK(c, launch_decode(a, grid, st, e0, e1));
     return finish_launch(c, st);
 }
 
@@ -634,7 +719,9 @@ hash_call(qhuff_ctx *c, const uint8_t *in, const uint32_t *off, uint32_t n,
     a.n = n;
     a.seed = seed;
     a.pairs = pairs ? 1u : 0u;
-    HIPCHK(c, launch_hash(a, c->hash_grid, (hipStream_t) stream));
+    hipEvent_t e0, e1;
+    timing_slot(c, QHUFF_KIND_HASH, &e0, &e1);
+    HIPCHK(c, launch_hash(a, c->hash_grid, (hipStream_t) stream, e0, e1));
     return QHUFF_OK;
 }
 
@@ -894,7 +981,11 @@ qhuff_encode_batch_host(qhuff_ctx *c, const uint8_t *in,
 {
     if (mode != 0 && mode != 3 && mode != 5 && mode != 7)
         return QHUFF_EINVAL;
-    if (c && c->svc && in_off && svc_fits(in_off, n))
+    // with a service attached the context may be shared between threads
+    // (qhuff_lsqpack_set_context): every call goes through svc_call, which
+    // serialises the ones too large for a slot on the context's host path
+    // (host_batch shares the context's staging buffers, streams and events)
+    if (c && c->svc)
         return svc_call(c->svc, true, in, in_off, n, mode, out, out_off, nullptr);
     return host_batch(c, true, in, in_off, n, mode, out, out_off, nullptr);
 }
@@ -904,7 +995,7 @@ qhuff_decode_batch_host(qhuff_ctx *c, const uint8_t *in,
                         const uint32_t *in_off, uint32_t n, uint8_t *out,
                         uint32_t *out_off, uint8_t *status)
 {
-    if (c && c->svc && in_off && svc_fits(in_off, n))
+    if (c && c->svc)                      // (see qhuff_encode_batch_host)
         return svc_call(c->svc, false, in, in_off, n, 0, out, out_off, status);
     return host_batch(c, false, in, in_off, n, 0, out, out_off, status);
 }
@@ -1093,6 +1184,13 @@ qhuff_svc_close(qhuff_svc *v)
     delete v;
 }
 
+// (qhuff_shim.cpp) whether ctx has the low-latency service attached
+bool
+qhuff::ctx_has_service(const qhuff_ctx *c)
+{
+    return c && c->svc;
+}
+
 extern "C" int
 qhuff_svc_stats(qhuff_svc *v, uint64_t *served, uint64_t *launches,
                 uint64_t *fallbacks)
@@ -1108,25 +1206,50 @@ qhuff_svc_stats(qhuff_svc *v, uint64_t *served, uint64_t *launches,
     return QHUFF_OK;
 }
 
+// Slot states (qhuff_svc::busy): free, taken by a call, or orphaned -- its
+// request was posted but the call gave up on it (an error while waiting);
+// an orphaned slot is free again once its done word shows that request.
+constexpr uint32_t kSlotFree = 0, kSlotTaken = 1, kSlotOrphan = 2;
+
 // take a free slot (spinning / yielding while none is); try_only: return
-// n_slots at once if none is free
+// n_slots at once if none is free.  A blocking take gives up after 10 s
+// (every slot held by calls that never finish, e.g. a service that cannot
+// run): it returns n_slots then too, and the caller reports QHUFF_EDEVICE.
 static uint32_t
 svc_take(qhuff_svc *v, bool try_only)
 {
     uint32_t k = v->next_slot.fetch_add(1, std::memory_order_relaxed) % v->n_slots;
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t tries = 0;; ++tries)
     {
-        uint32_t z = 0;
-        if (v->busy[k].compare_exchange_strong(z, 1, std::memory_order_acquire))
+        uint32_t z = kSlotFree;
+        if (v->busy[k].compare_exchange_strong(z, kSlotTaken,
+                                               std::memory_order_acquire))
             return k;
+        if (z == kSlotOrphan
+            && __atomic_load_n(&svc_hdr(v, k)->done, __ATOMIC_ACQUIRE) == v->seq[k]
+            && v->busy[k].compare_exchange_strong(z, kSlotTaken,
+                                                  std::memory_order_acquire))
+            return k;                            // its abandoned request is done
         k = (k + 1) % v->n_slots;
         if (tries % v->n_slots == v->n_slots - 1)
         {
             if (try_only)
                 return v->n_slots;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                return v->n_slots;
             std::this_thread::yield();
         }
     }
+}
+
+// a call that stops waiting for slot k's request sq: free the slot if the
+// request is done, else leave it orphaned (svc_take frees it once it is)
+static void
+svc_abandon(qhuff_svc *v, uint32_t k, uint32_t sq)
+{
+    const bool done = __atomic_load_n(&svc_hdr(v, k)->done, __ATOMIC_ACQUIRE) == sq;
+    v->busy[k].store(done ? kSlotFree : kSlotOrphan, std::memory_order_release);
 }
 
 // write strings [s0, s1) of the call into slot k and post it; returns the
@@ -1252,7 +1375,13 @@ svc_call(qhuff_svc *v, bool enc, const uint8_t *in, const uint32_t *in_off,
                 ++s1;
             const uint32_t k = svc_take(v, np > 0);
             if (k == v->n_slots)
-                break;
+            {
+                if (np > 0)
+                    break;                       // a partial round: go on
+                snprintf(c->err_msg, sizeof(c->err_msg),
+                         "service: no request slot freed within 10 s");
+                return QHUFF_EDEVICE;
+            }
             slot[np] = k;
             sq[np] = svc_post(v, k, enc, in, in_off, s0, s1, mode);
             p0[++np] = s1;
@@ -1262,19 +1391,24 @@ svc_call(qhuff_svc *v, bool enc, const uint8_t *in, const uint32_t *in_off,
         if (steady_ns() - v->last_done_ns.load(std::memory_order_relaxed)
                 > v->fresh_ns)
             rc = svc_ensure_running(v);
-        for (uint32_t j = 0; j < np && !rc; ++j)
+        for (uint32_t j = 0; j < np; ++j)
         {
-            rc = svc_wait(v, slot[j], sq[j]);
             if (!rc)
+                rc = svc_wait(v, slot[j], sq[j]);
+            if (rc)
             {
-                const uint32_t a = p0[j], m = p0[j + 1] - a;
-                base += svc_collect(v, slot[j], enc, m, base, out, out_off + a,
-                                    enc ? nullptr : status + a);
-                v->busy[slot[j]].store(0, std::memory_order_release);
+                // this piece and the rest of the round are abandoned: their
+                // slots come back once their requests are done
+                svc_abandon(v, slot[j], sq[j]);
+                continue;
             }
+            const uint32_t a = p0[j], m = p0[j + 1] - a;
+            base += svc_collect(v, slot[j], enc, m, base, out, out_off + a,
+                                enc ? nullptr : status + a);
+            v->busy[slot[j]].store(kSlotFree, std::memory_order_release);
         }
         if (rc)
-            return rc;                           // (unfinished slots stay taken)
+            return rc;
     }
     out_off[n] = base;
     v->served.fetch_add(1, std::memory_order_relaxed);

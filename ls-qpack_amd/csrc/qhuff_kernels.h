@@ -141,10 +141,16 @@ glb(T *p)
     return (QH_GLB T *) p;
 }
 
-hipError_t launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st);
-hipError_t launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st);
-hipError_t launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st);
+// ev0 / ev1 non-null: the launch records its own start / stop time in them
+// (hipExtLaunchKernelGGL: the dispatch's timestamps, no extra queue packets)
+hipError_t launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st,
+                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+hipError_t launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st,
+                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+hipError_t launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st,
+                       hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t hash_occupancy(int *blocks_per_cu);
+int hash_waves_per_block();
 hipError_t encode_occupancy(int *blocks_per_cu);
 hipError_t decode_occupancy(int *blocks_per_cu);
 size_t encode_lds_bytes();
@@ -153,6 +159,7 @@ int encode_waves_per_block();
 int decode_waves_per_block();
 uint32_t decode_tile_strings();            // strings per decode tile
 hipError_t launch_service(const SvcArgs &a, uint32_t grid, hipStream_t st);
+bool ctx_has_service(const qhuff_ctx *c);   // (qhuff_host.cpp)
 int service_waves_per_block();
 size_t service_lds_bytes();
 

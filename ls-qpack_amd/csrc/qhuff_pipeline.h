@@ -153,18 +153,20 @@ wait_vm_all()
 // (n_g waves of the workgroup in group g).  Three tickets per wave when the
 // tiles cover three per wave of the whole grid (the third replaces the
 // wave's own first claim, whose burst of ~3,000 returning adds the first
-// iteration would wait for), two when they cover two, else one (a small
-// batch then gets one tile per wave, not several per wave of the first
-// workgroups to start); a ticket not claimed here is kClaimNow: the wave
-// claims it itself once it runs, like every later one (a tile fixed to
-// whichever workgroup claimed it would need the whole grid resident: with
-// only some workgroups resident, e.g. beside another context, a group's
-// tickets could run ahead of another's and the look-backs above the gap
-// wait for tiles no running wave can claim).  Spread launches
-// (Coord::spread > 0, batches of at most one tile per wave of the grid,
-// qhuff_host.cpp grid_for): workgroup b's thread 0 adds `spread` to
-// counter 0 alone and its first `spread` waves take those tiles, one each;
-// the claimed tiles are always a prefix, so the same holds.
+// iteration would wait for), else two; a ticket not claimed here is
+// kClaimNow: the wave claims it itself once it runs, like every later one.
+// Every wave goes on claiming until a claim lands past the end, so no
+// ticket of any group is left to a workgroup that is not running -- a tile
+// fixed to whichever workgroup claimed it would need the whole grid
+// resident: with only some workgroups resident, e.g. beside another
+// context, a group's tickets could run ahead of another's and the
+// look-backs above the gap wait for tiles no running wave can claim.  (The
+// one-ticket-per-wave launch of rounds 2-3, where no wave claimed again,
+// had exactly that hole; it is gone.)  Batches of at most one tile per wave
+// of the grid are spread instead (Coord::spread > 0, qhuff_host.cpp
+// grid_for): workgroup b's thread 0 adds `spread` to counter 0 alone and
+// its first `spread` waves take those tiles, one each; the claimed tiles
+// are always a prefix, so the same holds.
 constexpr uint32_t kClaimNow = 0xffffffffu;   // ticket: claim it in the wave
                                               // (tile_pipeline)
 struct BlockTickets
@@ -183,13 +185,13 @@ tick_group_waves(uint32_t q)
          ? ((uint32_t) kWaves - 1 - first) / kTickGroups + 1 : 0u;
 }
 
-// tickets claimed per wave in the prologue
+// tickets claimed per wave in the prologue (ticket-group launches hold more
+// tiles than the grid has waves: smaller batches are spread)
 __device__ __forceinline__ uint32_t
 block_claims_per_wave(const Coord &c, uint32_t maxper)
 {
     const uint64_t g = (uint64_t) gridDim.x * kWaves;
-    return (uint64_t) c.n_tiles >= 3 * g && maxper >= 3 ? 3u
-         : (uint64_t) c.n_tiles > g ? 2u : 1u;
+    return (uint64_t) c.n_tiles >= 3 * g && maxper >= 3 ? 3u : 2u;
 }
 
 // the atomic of this thread's group share (threads 0..kTickGroups-1; its
@@ -301,9 +303,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     // ticket of the third iteration
     typename P::Offs o_cur, o_nxt, o_nn;
     o_cur.load(in_off, (uint64_t) t * TS, cnt_of(t));
-    // one ticket per wave from the workgroup claim only when the grid's
-    // waves cover every tile (block_claims_per_wave): this wave's one tile
-    // is then its last, with no claim after it
+    // (a spread launch's wave has one tile and no ticket after it)
     uint32_t tn = k1 == kClaimNow ? 0xffffffffu : tk.tile_of_u(k1);
     o_nxt.load(in_off, (uint64_t) clamp(tn) * TS, cnt_of(clamp(tn)));
     // a wave claims another tile only while its next one is real: a claimed
@@ -504,13 +504,9 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     for (int i = 0; i < D; ++i)
         if (pend[i].valid)
             flush_at(i, ld[i], ~0u);
-    // Small batches: once its tile is stored the wave claims the next, coded
-    // by the (out-of-line) slow path, until a ticket past the end -- every
-    // tile below a claimed one stays held by a running wave or claimable by
-    // one, whatever the residency, and nobody waits for a claim in the
-    // prologue (~3,000 returning adds there cost a one-round launch ~10 us:
-    // 24.3 -> 34.8 us, profiles/r02_k vs r03_u scaling.txt).  Rare: with
-    // every workgroup resident the first claim is already past the end.
+    // (The wave claimed until a claim landed past the end, so every ticket
+    // of its group is taken, by running waves: see BlockTickets.  A spread
+    // launch hands out a prefix of the tiles, one per wave.)
 }
 
 }  // namespace qhuff

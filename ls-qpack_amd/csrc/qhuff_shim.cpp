@@ -24,6 +24,10 @@
 #include "qhuff_fastwalk.h"
 #include "qhuff_tables.h"
 
+namespace qhuff {
+bool ctx_has_service(const qhuff_ctx *c);   // (qhuff_host.cpp)
+}
+
 namespace {
 
 std::atomic<qhuff_huff_decode_full_fn> g_full{nullptr};
@@ -194,6 +198,11 @@ qhuff_lsqpack_set_device(int device)
 extern "C" int
 qhuff_lsqpack_set_context(qhuff_ctx *ctx)
 {
+    // a shared context is thread-safe only through its service (qhuff_host.cpp
+    // svc_call): without one, concurrent calls would race on the context's
+    // host-path staging buffers and streams
+    if (ctx && !qhuff::ctx_has_service(ctx))
+        return QHUFF_EINVAL;
     g_shared.store(ctx, std::memory_order_release);
     return QHUFF_OK;
 }

@@ -35,12 +35,15 @@ EXPORTS = (
     "qhuff_frame_literal", "qhuff_xxh32_headers_host",
     "qhuff_svc_open", "qhuff_svc_close", "qhuff_svc_encode",
     "qhuff_svc_decode", "qhuff_svc_stats",
+    "qhuff_timing_enable", "qhuff_timing_read",
     # include/qhuff_lsqpack.h
     "qhuff_lsqpack_enc_enc_str", "qhuff_lsqpack_huff_decode",
     "qhuff_lsqpack_set_decode_full", "qhuff_lsqpack_set_device",
     "qhuff_lsqpack_set_context",
 )
 EPROTO, ETRUNC = -71, -61
+TIMING_SLOTS = 256                        # QHUFF_TIMING_SLOTS
+KIND_ENCODE, KIND_DECODE, KIND_HASH = 0, 1, 2
 LIT_NAME, LIT_VALUE = 1, 2
 
 XXH_SEED = 39378473                       # LSQPACK_XXH_SEED, lsqpack.c:623
@@ -187,6 +190,11 @@ def lib():
         L.qhuff_svc_stats.argtypes = [vp, C.POINTER(C.c_uint64),
                                       C.POINTER(C.c_uint64),
                                       C.POINTER(C.c_uint64)]
+        L.qhuff_timing_enable.restype = C.c_int
+        L.qhuff_timing_enable.argtypes = [vp, C.c_int]
+        L.qhuff_timing_read.restype = C.c_int
+        L.qhuff_timing_read.argtypes = [vp, u32p, C.POINTER(C.c_double),
+                                        C.c_uint32]
         L.qhuff_frame_literal.restype = C.c_int
         L.qhuff_frame_literal.argtypes = [C.c_uint, vp, C.c_size_t,
                                           C.c_char_p, C.c_uint, C.c_char_p,
@@ -347,6 +355,22 @@ class Codec:
         """Synchronise and return (then clear) the sticky device error word
         (0 = none, 1 = a look-back wait gave up)."""
         return int(lib().qhuff_device_error(self._ctx))
+
+    def timing(self, on=True):
+        """qhuff_timing_enable: time every later launch of this context by
+        its dispatch's own start / stop timestamps."""
+        self._check(lib().qhuff_timing_enable(self._ctx, 1 if on else 0),
+                    "qhuff_timing_enable")
+
+    def timing_read(self, max_launches=TIMING_SLOTS):
+        """qhuff_timing_read -> list of (kind, microseconds) of the launches
+        timed since timing() or the last read, oldest first (KIND_*)."""
+        kinds = (C.c_uint32 * max_launches)()
+        us = (C.c_double * max_launches)()
+        n = lib().qhuff_timing_read(self._ctx, kinds, us, max_launches)
+        if n < 0:
+            self._check(n, "qhuff_timing_read")
+        return [(int(kinds[i]), float(us[i])) for i in range(n)]
 
     def _check(self, rc, what):
         if rc != OK:

@@ -107,12 +107,15 @@ def test_one_context_two_streams(batch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [100_000, 150_000])
+@pytest.mark.parametrize("n", [100_000, 150_000, 196_700, 400_000])
 def test_two_contexts_concurrent_small(n):
-    """Batches of at most one tile per wave (the single-ticket prologue,
-    ADVICE r02): two contexts on two streams, several rounds back to back.
-    Each wave claims its second ticket itself, so whichever workgroups are
-    resident can fill a gap in any ticket group: no spin-limit error."""
+    """Two contexts on two streams, several rounds back to back, at batch
+    sizes around one round of the grid (W = 3,072 waves on 256 CUs): spread
+    launches (100k, 150k strings: at most one tile per wave) and ticket-group
+    launches just past one and two rounds (196,700 strings = W + 1 tiles,
+    400k), where every wave claims until a claim lands past the end -- so
+    whichever workgroups are resident can fill a gap in any ticket group
+    (VERDICT r03 item 6): no spin-limit error, bit-exact."""
     import torch
     import qhuff
     data, off = qhuff.synth_batch(n, seed=n)

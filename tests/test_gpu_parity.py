@@ -286,8 +286,10 @@ def _launch_shape_check(c, n, seed):
 def test_launch_shapes(codec):
     """Batch sizes around the launch-shape boundaries (qhuff_host.cpp
     grid_for): spread launches (one tile per wave, one workgroup per tile up
-    to the grid: 1..W tiles) and ticket-group launches with one, two and
-    three prologue tickets per wave (W = the resident grid's waves)."""
+    to the grid: 1..W tiles) and ticket-group launches with two and three
+    prologue tickets per wave (W = the resident grid's waves).  (The
+    one-ticket ticket-group launch and its QHUFF_NO_SPREAD switch are gone:
+    VERDICT r03 item 6.)"""
     n_cu = torch.cuda.get_device_properties(0).multi_processor_count
     W = n_cu * 12
     tiles = sorted({1, 7, 8, 9, n_cu - 1, n_cu, n_cu + 1, 4 * n_cu + 3,
@@ -296,27 +298,6 @@ def test_launch_shapes(codec):
         for n in (64 * t, 64 * t - 37):
             if n > 0:
                 _launch_shape_check(codec, n, seed=100 + 2 * i + (n % 2))
-
-
-def test_launch_shapes_no_spread():
-    """QHUFF_NO_SPREAD=1 (read when a context is created): batches the grid
-    covers fill whole workgroups instead; same results."""
-    import qhuff
-    old = os.environ.get("QHUFF_NO_SPREAD")
-    os.environ["QHUFF_NO_SPREAD"] = "1"
-    try:
-        c = qhuff.Codec(0)
-    finally:
-        if old is None:
-            del os.environ["QHUFF_NO_SPREAD"]
-        else:
-            os.environ["QHUFF_NO_SPREAD"] = old
-    try:
-        n_cu = torch.cuda.get_device_properties(0).multi_processor_count
-        for t in (1, 9, n_cu + 1, n_cu * 12):
-            _launch_shape_check(c, 64 * t - 5, seed=7 + t)
-    finally:
-        c.close()
 
 
 def test_full_size_round_trip(codec):

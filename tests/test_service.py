@@ -259,3 +259,80 @@ def test_svc_shared_context_for_lsqpack_shims(codec, svc):
         L.qhuff_lsqpack_set_context(None)
     assert not errors, errors[:3]
     assert svc.stats()[0] >= served0 + 4 * 40 * 2
+
+
+@pytest.mark.parametrize("size", [3073, 20000, 65536])
+def test_svc_single_long_string(svc, size):
+    """one string longer than the 3 KB stage: the service's scratch path
+    (input copied to the slot's device scratch, the tile loop, results
+    copied back) -- valid strings in every mode and back, and invalid
+    Huffman input of the same sizes"""
+    rng = random.Random(size)
+    tok = list(b"abcdefghijklmnopqrstuvwxyz0123456789-_.:/=")
+    s = bytes(rng.choice(tok) for _ in range(size))
+    data, off = pack([s], base=rng.randint(0, 5))
+    served0, _, fb0 = svc.stats()
+    for mode in (0, 3, 5, 7):
+        check_enc(svc, data, off, mode)
+    enc, eo = check_enc(svc, data, off, 0)
+    assert int(eo[-1]) <= MAX_B                     # the payload fits a slot
+    check_dec(svc, enc, eo)
+    # invalid: the payload with its last byte's padding broken, and random
+    # bytes (EOS or bad padding somewhere)
+    bad = enc.copy()
+    bad[int(eo[-1]) - 1] &= 0x7f
+    _, _, st = check_dec(svc, bad, eo)
+    junk = np.frombuffer(bytes(rng.getrandbits(8) for _ in range(size)),
+                         dtype=np.uint8).copy()
+    check_dec(svc, junk, np.array([0, size], dtype=np.uint32))
+    served1, _, fb1 = svc.stats()
+    assert fb1 == fb0 and served1 >= served0 + 8   # none took the host path
+
+
+def test_svc_shared_context_long_strings_threaded(codec, svc):
+    """calls too large for a slot (> 64 KB) on a shared context
+    go through the service's fallback lock, so threads mixing them with
+    small calls still get bit-exact results"""
+    import qhuff
+    L = qhuff.lib()
+    assert L.qhuff_lsqpack_set_context(codec._ctx) == qhuff.OK
+    errors = []
+
+    def worker(t):
+        try:
+            rng = random.Random(50 + t)
+            for i in range(6):
+                k = MAX_B + 1 + rng.randint(0, 5000) if i % 2 else \
+                    rng.randint(0, 200)
+                s = bytes(rng.choice(b"abcdefgh-./:0123") for _ in range(k))
+                want = O.enc_enc_str(7, s)
+                assert qhuff.lsqpack_enc_enc_str(7, s, dst_len=len(want) + 8) \
+                    == want
+                h = O.huffman_enc(s)
+                st, dst = qhuff.lsqpack_huff_decode(h, len(s) + 1)[:2]
+                assert st == 0 and dst == s
+        except Exception as e:                      # noqa: BLE001
+            errors.append(repr(e))
+
+    try:
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+    finally:
+        L.qhuff_lsqpack_set_context(None)
+    assert not errors, errors[:3]
+
+
+def test_set_context_requires_service():
+    """a context without a service cannot be shared (its host path is not
+    thread-safe): QHUFF_EINVAL, and the default contexts stay in use"""
+    import qhuff
+    c = qhuff.Codec(0)
+    try:
+        L = qhuff.lib()
+        assert L.qhuff_lsqpack_set_context(c._ctx) == qhuff.EINVAL
+        assert qhuff.lsqpack_enc_enc_str(5, b"dude") == O.enc_enc_str(5, b"dude")
+    finally:
+        c.close()

@@ -172,13 +172,18 @@ def main():
     for _ in range(3):
         h, ho = codec.encode(d, o, 0)
     torch.cuda.synchronize()
-    report("encode", codec.profile_read())
+    pe = codec.profile_read()
+    report("encode", pe)
     hb = int(ho[-1].item())
     h = h[:hb].clone()
     for _ in range(3):
         codec.decode(h, ho)
     torch.cuda.synchronize()
-    report("decode", codec.profile_read())
+    pd = codec.profile_read()
+    report("decode", pd)
+    if os.environ.get("RAW"):
+        # raw stamps for offline analysis (tools/tail_report.py)
+        np.savez_compressed(os.environ["RAW"], encode=pe, decode=pd)
     codec.close()
 
 
