@@ -53,10 +53,12 @@ int qhuff_lsqpack_enc_enc_str(unsigned prefix_bits, unsigned char *dst,
  *   otherwise (resumed or non-final chunks: streaming input): the registered
  *   streaming decoder (the reference's own lsqpack_huff_decode_full,
  *   lsqpack.c:3443, always exported); with none registered: ERROR.
- * (qhuff_huff_decode_ex in qhuff.h is the same on an explicit context.)
- * One deviation: an invalid string whose output overflows dst before the
- * point where the reference detects the error returns ERROR where the
- * reference returns END_DST first (the caller's retry reaches the ERROR). */
+ *   An invalid string gets the reference's answer too: ERROR -- or END_DST
+ *   (the same byte-boundary back-off) when dst runs out before the
+ *   reference reaches the error, and the streaming decoder's result where
+ *   a code longer than 16 bits comes first (the GPU decodes the bytes
+ *   before the error, qhuff_fastwalk.h replays the reference over them).
+ * (qhuff_huff_decode_ex in qhuff.h is the same on an explicit context.) */
 struct qhuff_decode_retval
 qhuff_lsqpack_huff_decode(const unsigned char *src, int src_len,
                           unsigned char *dst, int dst_len,

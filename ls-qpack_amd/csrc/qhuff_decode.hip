@@ -34,8 +34,9 @@
 
 namespace qhuff {
 
-using DecPolicy = DecPolicyT<DecSmem>;
-
+// Keep: the per-string entry points' kernel (DecPolicyT); a template
+// parameter, so the batch kernel's code and registers are untouched
+template <bool Keep>
 __global__ __launch_bounds__(64 * kWaves) void
 qhuff_decode_kernel(DecArgs a)
 {
@@ -68,7 +69,8 @@ qhuff_decode_kernel(DecArgs a)
     // __syncthreads() would drain them)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
-    DecPolicy pol{a.in, sm, &sm->w[__builtin_amdgcn_readfirstlane(tid >> 6)], 0};
+    DecPolicyT<DecSmem, Keep> pol{a.in, sm,
+                                  &sm->w[__builtin_amdgcn_readfirstlane(tid >> 6)], 0};
     uint32_t t0, k1, k2;
     wave_tickets(a.c, tk, &sm->tk, &t0, &k1, &k2);
     auto tables = [&]() {
@@ -92,14 +94,17 @@ qhuff_decode_kernel(DecArgs a)
 
 hipError_t
 launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st, hipEvent_t ev0,
-              hipEvent_t ev1)
+              hipEvent_t ev1, bool keep)
 {
-    if (ev0)
-        hipExtLaunchKernelGGL(qhuff_decode_kernel, dim3(grid), dim3(64 * kWaves), 0, st,
-                              ev0, ev1, 0, a);
+    if (keep)
+        hipLaunchKernelGGL(qhuff_decode_kernel<true>, dim3(grid),
+                           dim3(64 * kWaves), 0, st, a);
+    else if (ev0)
+        hipExtLaunchKernelGGL(qhuff_decode_kernel<false>, dim3(grid),
+                              dim3(64 * kWaves), 0, st, ev0, ev1, 0, a);
     else
-        hipLaunchKernelGGL(qhuff_decode_kernel, dim3(grid), dim3(64 * kWaves),
-                           0, st, a);
+        hipLaunchKernelGGL(qhuff_decode_kernel<false>, dim3(grid),
+                           dim3(64 * kWaves), 0, st, a);
     return hipGetLastError();
 }
 
@@ -107,7 +112,7 @@ hipError_t
 decode_occupancy(int *blocks_per_cu)
 {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        blocks_per_cu, reinterpret_cast<const void *>(qhuff_decode_kernel),
+        blocks_per_cu, reinterpret_cast<const void *>(qhuff_decode_kernel<false>),
         64 * kWaves, 0);
 }
 
@@ -127,7 +132,7 @@ size_t
 decode_lds_bytes()
 {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(qhuff_decode_kernel))
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(qhuff_decode_kernel<false>))
             != hipSuccess)
         return 0;
     return fa.sharedSizeBytes;

@@ -172,7 +172,9 @@ main_step(bool act, uint32_t d, uint32_t &hi, uint32_t &lo, uint32_t &bits,
 
 // Decode one string whose bits are [bit0, bitend) of the big-endian dword
 // stream `src`; emitted bytes go through `emit`.  Returns the number of
-// output bytes, or -1 for a rejected string.  Three wave-uniform phases:
+// output bytes, or -1 - k for a rejected string (k: the bytes emitted before
+// the error, every symbol before the EOS code or before the bad padding).
+// Three wave-uniform phases:
 //   1. while every lane has >= 32 real bits ahead: ungated steps;
 //   2. while some lane does: steps predicated on the lane's own state;
 //   3. the last < 32 bits, padded with ones, with the D3 tail rule.
@@ -255,10 +257,10 @@ decode_string(const Src &src, uint32_t bit0, uint32_t bitend,
         rem -= c;
         fin = fin | over | eos | (rem == 0);
     } while (__builtin_amdgcn_ballot_w64(!fin));
-    return bad ? -1 : (int) emit.n;
+    return bad ? -1 - (int) emit.n : (int) emit.n;
 }
 
-// Lean variant used by the staged (LDS) path.  The bit stream sits in two
+// Lean variant used by the staged (LDS) path (same return value).  The bit stream sits in two
 // dwords A:B with a position t: the 32-bit window is alignbit(A, B, t) --
 // ((A:B) >> t), the next bit at A's bit 31 - (32 - t) -- valid for t in
 // [0, 31] (t = 0: the window is B).  Consuming c bits lowers t; when it goes
@@ -395,7 +397,7 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         bad |= (live & !pad_ok) ? 1u : 0u;
     }
     emit.finish();
-    return bad ? -1 : (int) emit.n;
+    return bad ? -1 - (int) emit.n : (int) emit.n;
 }
 
 // byte-granular arena sink: two unconditional byte stores per step, the
@@ -515,8 +517,9 @@ compact_wave(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
 // tile's output base comes from base_of(total) (the batch kernel's look-back,
 // or the service's running offset); its offsets and statuses go to t_off /
 // t_status (the tile's first string).  Returns base + total.  Out of line
-// (cold), state by value.
-template <class SM, class BaseOf>
+// (cold), state by value.  Keep: a rejected string's output is the bytes
+// decoded before its error (DecPolicyT).
+template <bool Keep, class SM, class BaseOf>
 __device__ __noinline__ uint64_t
 dec_slow_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
               uint32_t slot0, uint32_t cnt, TileOffs to, Span sp, uint32_t sz,
@@ -536,7 +539,7 @@ dec_slow_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
             CountEmit em{0};
             r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted, em);
         }
-        sz = r < 0 ? 0u : (uint32_t) r;
+        sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
         st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
     }
     const uint32_t incl = wave_incl_scan(sz);
@@ -550,7 +553,7 @@ dec_slow_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
         for (uint32_t i = 0; i < sz; ++i)
             ((QH_GLB uint8_t *) dst)[i] = sa[i];
     }
-    else if (valid && st == QHUFF_DEC_OK && sz)
+    else if (valid && (Keep || st == QHUFF_DEC_OK) && sz)
     {
         GlobalEmit em{dst, 0};
         decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted, em);
@@ -564,8 +567,11 @@ dec_slow_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
 }
 
 // the decode side of the wave pipeline (qhuff_pipeline.h, qhuff_service.hip);
-// SM: the workgroup's LDS (win, sorted)
-template <class SM>
+// SM: the workgroup's LDS (win, sorted).  Keep (the kernel the per-string
+// entry points use to replay where the reference stops on an invalid
+// string, qhuff_shim.cpp): a rejected string keeps, as its output, the bytes
+// decoded before the error; its status is QHUFF_DEC_ERROR all the same.
+template <class SM, bool Keep = false>
 struct DecPolicyT
 {
     static constexpr bool kStatus = true;
@@ -610,7 +616,7 @@ struct DecPolicyT
             r = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted,
                                   em);
         }
-        *sz = r < 0 ? 0u : (uint32_t) r;
+        *sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
         *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
     }
     // arena -> the (dead) input stage, compacted
@@ -630,7 +636,7 @@ struct DecPolicyT
                                               uint64_t n)
     {
         const uint64_t s0 = (uint64_t) t * kTS;
-        const uint64_t end = dec_slow_tile(in, sm, wv, slot0, cnt, to, sp, sz,
+        const uint64_t end = dec_slow_tile<Keep>(in, sm, wv, slot0, cnt, to, sp, sz,
                                            st, out, out_off + s0, status + s0,
                                            LookBackBase{c, t});
         last_tile_end(c, t, end, out_off, n);
@@ -642,7 +648,7 @@ struct DecPolicyT
                                                      uint32_t *t_off,
                                                      uint8_t *t_status)
     {
-        return dec_slow_tile(in, sm, wv, slot0, cnt, to, sp, sz, st, out, t_off,
+        return dec_slow_tile<Keep>(in, sm, wv, slot0, cnt, to, sp, sz, st, out, t_off,
                              t_status, FixedBase{base});
     }
 };

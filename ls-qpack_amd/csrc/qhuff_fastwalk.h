@@ -13,6 +13,8 @@
 
 #include <stdint.h>
 
+#include "qhuff_tables.h"
+
 namespace qhuff {
 
 enum FastEnd : uint8_t
@@ -109,6 +111,138 @@ fast_walk(const uint8_t *len, uint32_t n, uint32_t src_len, uint32_t dst_len)
     return FastStop{kFastDone, d, src_len};
 back_off:
     // previous byte boundary (lsqpack.c:5442-5445, 5454-5457)
+    while ((avail & 7) && d > 0)
+        avail += len[--d];
+    return FastStop{end, d, R - (avail >> 3)};
+}
+
+// Canonical first code and count of every code length (RFC 7541 Appendix B,
+// kLen), for code_completes().
+struct CanonLens
+{
+    uint32_t first[31], count[31];
+};
+
+constexpr CanonLens
+make_canon_lens()
+{
+    CanonLens c{};
+    for (int s = 0; s < 257; ++s)
+        c.count[kLen[s]]++;
+    uint32_t next = 0;
+    for (int L = 1; L <= 30; ++L)
+    {
+        next <<= 1;
+        c.first[L] = next;
+        next += c.count[L];
+    }
+    return c;
+}
+
+constexpr CanonLens kCanonLens = make_canon_lens();
+
+// whether the left-aligned bits of w start with a whole code of at most
+// maxbits bits (the question hdecs[] answers for a window, lsqpack.c:5371)
+inline bool
+code_completes(uint32_t w, unsigned maxbits)
+{
+    for (unsigned L = 1; L <= maxbits && L <= 30; ++L)
+        if (kCanonLens.count[L]
+            && (w >> (32 - L)) - kCanonLens.first[L] < kCanonLens.count[L])
+            return true;
+    return false;
+}
+
+// bits [pos, pos + 32) of src (big-endian bit order), ones past src_len
+inline uint32_t
+bits_at(const uint8_t *src, uint32_t src_len, uint32_t pos)
+{
+    uint32_t w = 0;
+    for (unsigned k = 0; k < 32; ++k)
+    {
+        const uint32_t b = pos + k;
+        const uint32_t bit = b < 8 * src_len ? (src[b >> 3] >> (7 - (b & 7))) & 1
+                                             : 1u;
+        w = (w << 1) | bit;
+    }
+    return w;
+}
+
+// The same replay for an INVALID string (the GPU rejected it): len[0..n)
+// are the code lengths of the symbols decoded before the error, followed,
+// when the error is the EOS code in the data, by a 30 for the EOS code
+// itself -- no window of the fast decoder holds it, so the walk takes the
+// slow path there, as the reference does (its nibble decoder then finds the
+// EOS, lsqpack.c:3480-3497).  Otherwise the error is the padding, found
+// only after the last window (lsqpack.c:5362-5426): end kFastDone means the
+// reference returns ERROR; kFastDstEnded / kFastSlow as in fast_walk.  In
+// that last window the reference's table decodes, after the string's last
+// whole codes, one more code if the padded bits complete one within the
+// window -- a code running past the input: ERROR before any room check
+// (lsqpack.c:5373-5378); otherwise its symbols are written, or do not fit
+// (END_DST, 5398-5399).
+inline FastStop
+fast_walk_invalid(const uint8_t *len, uint32_t n, const uint8_t *src,
+                  uint32_t src_len, uint32_t dst_len)
+{
+    uint32_t R = 0;
+    unsigned avail = 0;
+    uint32_t d = 0;
+    FastEnd end = kFastDone;
+    for (;;)
+    {
+        if (R >= src_len)
+            break;
+        while (R < src_len && avail <= 56)
+        {
+            ++R;
+            avail += 8;
+        }
+        if (dst_len - d >= 64 / 5 && avail >= 16)
+        {
+            unsigned k, used;
+            do
+            {
+                k = fast_window(len, n, d, 16, &used);
+                d += k;
+                avail -= used;
+            } while (avail >= 16 && k);
+            if (avail < 16)
+                continue;
+            end = kFastSlow;
+            goto back_off;
+        }
+        while (avail >= 16)
+        {
+            unsigned used;
+            const unsigned k = fast_window(len, n, d, 16, &used);
+            if (k && d + k <= dst_len)
+            {
+                d += k;
+                avail -= used;
+            }
+            else
+            {
+                end = d + k > dst_len ? kFastDstEnded : kFastSlow;
+                goto back_off;
+            }
+        }
+    }
+    if (avail >= 5)
+    {
+        unsigned used;
+        const unsigned k = fast_window(len, n, d, avail, &used);
+        if (k < 3 && code_completes(bits_at(src, src_len, 8 * R - avail + used),
+                                    16 - used))
+            return FastStop{kFastDone, 0, 0};            // ERROR
+        if (k && d + k > dst_len)
+        {
+            end = kFastDstEnded;
+            goto back_off;
+        }
+    }
+    return FastStop{kFastDone, 0, 0};                    // ERROR (padding)
+back_off:
     while ((avail & 7) && d > 0)
         avail += len[--d];
     return FastStop{end, d, R - (avail >> 3)};

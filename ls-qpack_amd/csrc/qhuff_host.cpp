@@ -179,6 +179,9 @@ struct qhuff_ctx
     // the low-latency service attached by qhuff_svc_open (small host-path
     // calls on this context go through it)
     qhuff_svc *svc;
+    // decode launches keep a rejected string's bytes decoded before its error
+    // (qhuff::decode_keep_rejected, for qhuff_shim.cpp)
+    bool keep_rejected;
     // launch timing (qhuff_timing_enable): a start / stop event pair per
     // launch, a ring of the last QHUFF_TIMING_SLOTS launches
     hipEvent_t *tev;                     // [2 * QHUFF_TIMING_SLOTS], or null
@@ -694,7 +697,7 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     const uint32_t grid = grid_for(c, tiles, wpb, c->dec_grid, &a.c.spread);
     hipEvent_t e0, e1;
     timing_slot(c, QHUFF_KIND_DECODE, &e0, &e1);
-    HIPCHK(c, launch_decode(a, grid, st, e0, e1));
+    HIPCHK(c, launch_decode(a, grid, st, e0, e1, c->keep_rejected));
     return finish_launch(c, st);
 }
 
@@ -1189,6 +1192,28 @@ bool
 qhuff::ctx_has_service(const qhuff_ctx *c)
 {
     return c && c->svc;
+}
+
+// (qhuff_shim.cpp) one host-memory decode call whose rejected strings keep,
+// as their output, the bytes decoded before the error (the DecPolicyT Keep
+// kernel): the per-string entry points replay from them where the
+// reference's decoder stops on an invalid string.  Through the context's
+// host path, under the service's fallback lock when one is attached (the
+// context may then be shared between threads).
+int
+qhuff::decode_keep_rejected(qhuff_ctx *c, const uint8_t *in,
+                            const uint32_t *in_off, uint32_t n, uint8_t *out,
+                            uint32_t *out_off, uint8_t *status)
+{
+    if (!c)
+        return QHUFF_EINVAL;
+    std::unique_lock<std::mutex> lk;
+    if (c->svc)
+        lk = std::unique_lock<std::mutex>(c->svc->fallback_mu);
+    c->keep_rejected = true;
+    const int rc = host_batch(c, false, in, in_off, n, 0, out, out_off, status);
+    c->keep_rejected = false;
+    return rc;
 }
 
 extern "C" int

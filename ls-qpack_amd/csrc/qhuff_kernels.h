@@ -145,8 +145,11 @@ glb(T *p)
 // (hipExtLaunchKernelGGL: the dispatch's timestamps, no extra queue packets)
 hipError_t launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st,
                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// keep: the kernel that keeps a rejected string's bytes decoded before its
+// error (qhuff_shim.cpp)
 hipError_t launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st,
-                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
+                         bool keep = false);
 hipError_t launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st,
                        hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t hash_occupancy(int *blocks_per_cu);
@@ -160,6 +163,9 @@ int decode_waves_per_block();
 uint32_t decode_tile_strings();            // strings per decode tile
 hipError_t launch_service(const SvcArgs &a, uint32_t grid, hipStream_t st);
 bool ctx_has_service(const qhuff_ctx *c);   // (qhuff_host.cpp)
+int decode_keep_rejected(qhuff_ctx *c, const uint8_t *in,
+                         const uint32_t *in_off, uint32_t n, uint8_t *out,
+                         uint32_t *out_off, uint8_t *status);
 int service_waves_per_block();
 size_t service_lds_bytes();
 

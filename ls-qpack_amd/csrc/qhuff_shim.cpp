@@ -26,6 +26,9 @@
 
 namespace qhuff {
 bool ctx_has_service(const qhuff_ctx *c);   // (qhuff_host.cpp)
+int decode_keep_rejected(qhuff_ctx *c, const uint8_t *in,
+                         const uint32_t *in_off, uint32_t n, uint8_t *out,
+                         uint32_t *out_off, uint8_t *status);
 }
 
 namespace {
@@ -73,6 +76,78 @@ default_ctx()
 
 constexpr qhuff_decode_retval kErr = {QHUFF_HUFF_DEC_ERROR, 0, 0};
 
+
+// An invalid complete string (the GPU rejected it).  The reference reports
+// ERROR (n_dst = n_src = 0, lsqpack.c:5374-5425, 3482-3497) -- unless dst
+// runs out before it reaches the error, when it reports END_DST like for a
+// valid string (5438-5450) or its nibble decoder does (3469-3491) -- and
+// where a code longer than 16 bits sends the reference to that nibble
+// decoder (5452-5465), its result (ERROR with the n_dst / n_src it reached
+// when the end of the input is not a valid padding, 3502-3507) is what the
+// reference returns.  The GPU decodes the string again keeping the bytes
+// before the error (the Keep kernel), and fast_walk_invalid replays the
+// reference over their code lengths.
+qhuff_decode_retval
+rejected(qhuff_ctx *c, const unsigned char *src, int src_len,
+         unsigned char *dst, int dst_len, struct qhuff_huff_decode_state *state,
+         int final)
+{
+    std::vector<unsigned char> &buf = t_ctx.buf;
+    const uint32_t off[2] = {0, (uint32_t) src_len};
+    uint32_t oo[2] = {0, 0};
+    uint8_t st = QHUFF_DEC_OK;
+    if (qhuff::decode_keep_rejected(c, src, off, 1, buf.data(), oo, &st)
+            != QHUFF_OK || st != QHUFF_DEC_ERROR)
+        return kErr;
+    const unsigned n = oo[1];                // bytes before the error
+    std::vector<uint8_t> &lens = t_ctx.lens;
+    lens.resize(n + 1);
+    uint64_t pbits = 0;
+    for (unsigned i = 0; i < n; ++i)
+    {
+        lens[i] = qhuff::kLen[buf[i]];
+        pbits += lens[i];
+    }
+    // the EOS code right after them (else the padding is what is wrong)
+    const bool eos = pbits + 30 <= 8ull * (uint64_t) src_len
+                  && qhuff::bits_at(src, (uint32_t) src_len, (uint32_t) pbits)
+                         >> 2 == 0x3fffffffu;
+    if (eos)
+        lens[n] = 30;
+    const qhuff::FastStop fs = qhuff::fast_walk_invalid(
+        lens.data(), n + (eos ? 1 : 0), src, (uint32_t) src_len,
+        (uint32_t) dst_len);
+    if (fs.end == qhuff::kFastDone)
+        return kErr;
+    if (fs.n_dst)
+        memcpy(dst, buf.data(), fs.n_dst);
+    if (fs.end == qhuff::kFastSlow)
+    {
+        const qhuff_huff_decode_full_fn full = g_full.load();
+        if (full)
+        {
+            // the reference's nibble decoder from that byte (5452-5465)
+            qhuff_decode_retval rv = full(src + fs.n_src,
+                                          src_len - (int) fs.n_src,
+                                          dst + fs.n_dst,
+                                          dst_len - (int) fs.n_dst, state,
+                                          final);
+            if (rv.status == QHUFF_HUFF_DEC_OK
+                    || rv.status == QHUFF_HUFF_DEC_END_DST)
+            {
+                rv.n_dst += fs.n_dst;
+                rv.n_src += fs.n_src;
+            }
+            return rv;
+        }
+        // no streaming decoder registered: ERROR when every byte before the
+        // error fits, else the byte-boundary END_DST (as for valid strings)
+        if (n <= (unsigned) dst_len)
+            return kErr;
+    }
+    return qhuff_decode_retval{QHUFF_HUFF_DEC_END_DST, fs.n_dst, fs.n_src};
+}
+
 }  // namespace
 
 extern "C" struct qhuff_decode_retval
@@ -98,9 +173,10 @@ qhuff_huff_decode_ex(qhuff_ctx *c, const unsigned char *src, int src_len,
     uint8_t st = QHUFF_DEC_ERROR;
     const unsigned char dummy = 0;
     if (qhuff_decode_batch_host(c, src_len ? src : &dummy, off, 1, buf.data(),
-                                oo, &st) != QHUFF_OK
-            || st != QHUFF_DEC_OK)
-        return kErr;                         // n_dst = n_src = 0 (5374-5425)
+                                oo, &st) != QHUFF_OK)
+        return kErr;
+    if (st != QHUFF_DEC_OK)
+        return rejected(c, src, src_len, dst, dst_len, state, final);
     const unsigned n = oo[1];
     // the code lengths decide where the reference's fast decoder stops
     std::vector<uint8_t> &lens = t_ctx.lens;

@@ -209,3 +209,28 @@ def bench_pass(data, in_off, op, nthreads, slot_bytes=128):
     sink = C.c_ulonglong()
     return lib().oq_bench_pass(_p(data), _p(in_off), len(in_off) - 1, op,
                                nthreads, slot_bytes, C.byref(sink))
+
+
+def decoded_prefix(src: bytes):
+    """(symbols, eos): the symbols of src decoded before its error -- every
+    whole code before the EOS code, or before padding that cannot complete
+    one -- and whether the error is the EOS code.  A bit-level greedy decode
+    over the oracle's code table (test-side; what the GPU's Keep kernel
+    returns for a rejected string)."""
+    codes = {}
+    for s in range(257):
+        c, n = code_of(s)
+        codes[(n, c)] = s
+    bits = "".join(format(b, "08b") for b in src)
+    out, i = [], 0
+    while True:
+        for L in range(5, 31):
+            if i + L > len(bits):
+                return bytes(out), False
+            sym = codes.get((L, int(bits[i:i + L], 2)))
+            if sym is not None:
+                break
+        if sym == 256:
+            return bytes(out), True
+        out.append(sym)
+        i += L

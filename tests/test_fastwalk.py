@@ -91,3 +91,81 @@ def test_walk_random(walk, alpha, lo, hi, n):
     for _ in range(n):
         _check(walk, bytes(rng.choice(alpha)
                            for _ in range(rng.randint(lo, hi))))
+
+
+def _invalid_inputs(seed):
+    """Invalid complete strings of every D3 kind: the EOS code after a
+    prefix (short and long codes before it), padding of 8-23 ones, padding
+    that is not all ones, random bytes."""
+    rng = random.Random(seed)
+    eos = "1" * 30
+    out = []
+
+    def bits(s):
+        return "".join(format(O.code_of(b)[0], "0%db" % O.code_of(b)[1])
+                       for b in s)
+
+    def tob(b):
+        b += "1" * (-len(b) % 8)
+        return int(b, 2).to_bytes(len(b) // 8, "big")
+    for _ in range(60):
+        s = bytes(rng.choice(SHORT + MID + LONG) for _ in
+                  range(rng.randint(0, 30)))
+        t = bytes(rng.choice(SHORT) for _ in range(rng.randint(0, 6)))
+        out.append(tob(bits(s) + eos + bits(t)))                 # EOS
+        out.append(tob(bits(s) + "1" * rng.randint(8, 23)))      # long padding
+        pad = "".join(rng.choice("01") for _ in range(rng.randint(1, 7)))
+        if "0" in pad:
+            b = bits(s) + pad
+            if len(b) % 8 == 0:
+                out.append(int(b, 2).to_bytes(len(b) // 8, "big"))
+            else:
+                b += "1" * (-len(b) % 8)
+                out.append(int(b, 2).to_bytes(len(b) // 8, "big"))
+    for _ in range(300):
+        out.append(bytes(rng.randrange(256) for _ in range(rng.randint(1, 14))))
+    return [x for x in out if O.huff_decode(x)[0] == O.ERROR]
+
+
+def test_walk_invalid_every_dst_len(walk_invalid):
+    """fast_walk_invalid (the shim's replay for a string the GPU rejected)
+    over the symbols decoded before the error reproduces oq_huff_decode's
+    (status, n_dst, n_src) at every dst_len: ERROR, or END_DST where dst runs
+    out first, or the nibble decoder's result from the byte it names."""
+    inputs = _invalid_inputs(21)
+    assert len(inputs) > 200
+    for enc in inputs:
+        for dst_len in range(0, 8 * len(enc) // 5 + 3):
+            assert walk_invalid(enc, dst_len) == oracle(enc, dst_len), \
+                (enc.hex(), dst_len)
+
+
+@pytest.fixture(scope="module")
+def walk_invalid(walk):
+    L = C.CDLL(SO)
+    L.qh_fast_walk_invalid.restype = None
+    L.qh_fast_walk_invalid.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p,
+                                       C.c_uint32, C.c_uint32,
+                                       C.POINTER(C.c_uint32)]
+    lens = [O.code_of(s)[1] for s in range(256)]
+
+    def run(enc, dst_len):
+        prefix, eos = O.decoded_prefix(enc)
+        ln = bytes([lens[b] for b in prefix] + ([30] if eos else []))
+        out = (C.c_uint32 * 3)()
+        L.qh_fast_walk_invalid(ln, len(ln), enc, len(enc), dst_len, out)
+        end, n_dst, n_src = out
+        if end == 0:
+            return O.ERROR, 0, 0
+        if end == 1:
+            return O.END_DST, n_dst, n_src
+        rest = enc[n_src:]
+        s = C.create_string_buffer(rest, len(rest) + 1)
+        d = C.create_string_buffer(max(dst_len - n_dst, 1))
+        st = O.DecState(0, 0, 0)
+        rv = O.lib().oq_huff_decode_full(s, len(rest), d, dst_len - n_dst,
+                                         C.byref(st), 1)
+        if rv.status in (O.OK, O.END_DST):
+            return rv.status, rv.n_dst + n_dst, rv.n_src + n_src
+        return rv.status, rv.n_dst, rv.n_src
+    return run

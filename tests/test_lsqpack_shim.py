@@ -6,7 +6,8 @@ too small the shim returns what the reference's huff_decode_fast returns
 (END_DST with n_dst/n_src backed off to a byte boundary,
 lsqpack.c:5438-5450), or, where the reference falls into its nibble decoder
 (slow_path, lsqpack.c:5452-5465), hands the rest to the registered streaming
-decoder.  Here the registered decoder is the oracle's restatement of
+decoder -- for invalid strings as well (END_DST where dst runs out before the
+error, qhuff_fastwalk.h fast_walk_invalid).  Here the registered decoder is the oracle's restatement of
 lsqpack_huff_decode_full, so every (status, n_dst, n_src, dst) must equal
 the oracle's oq_huff_decode on the same arguments, for every dst_len.
 
@@ -102,14 +103,38 @@ def test_decode_random_every_dst_len(shim, alpha, lo, hi, n):
 
 @pytest.mark.gpu
 def test_decode_invalid_strings(shim):
-    """Random bytes: valid ones decode exactly; invalid ones are ERROR with
-    n_dst = n_src = 0 when dst is ample (the documented deviation only
-    concerns an invalid string with a dst too small for its output)."""
+    """Random bytes: valid ones decode exactly; invalid ones as the
+    reference reports them when dst is ample (ERROR, with the nibble
+    decoder's n_dst / n_src where a long code sent the reference there)."""
     rng = random.Random(7)
     for _ in range(300):
         src = bytes(rng.randrange(256) for _ in range(rng.randint(1, 12)))
         cap = 4 * len(src) + 8
         assert shim_decode(shim, src, cap) == oracle_decode(src, cap)
+
+
+@pytest.mark.gpu
+def test_decode_invalid_every_dst_len(shim):
+    """an invalid complete string at every dst_len --
+    the EOS code after short and long codes, padding of 8+ ones, padding
+    that is not all ones, random bytes, the reference's must-reject KATs --
+    gives oq_huff_decode's (status, dst, n_dst, n_src): END_DST where dst
+    runs out before the reference reaches the error, the nibble decoder's
+    result where a long code sends it there, else ERROR (the GPU's Keep
+    kernel returns the bytes before the error; qhuff_fastwalk.h
+    fast_walk_invalid replays the reference over them)."""
+    import test_fastwalk as TF
+    kat = json.load(open(os.path.join(GOLD, "kat_huff_decode.json")))
+    inputs = [bytes.fromhex(k["huff"]) for k in kat["decode_error"]]
+    inputs += TF._invalid_inputs(33)[:150]
+    n_end_dst = 0
+    for enc in inputs:
+        for dst_len in range(0, 8 * len(enc) // 5 + 3):
+            got = shim_decode(shim, enc, dst_len)
+            want = oracle_decode(enc, dst_len)
+            assert got == want, (enc.hex(), dst_len, got, want)
+            n_end_dst += want[0] == O.END_DST
+    assert n_end_dst > 100
 
 
 @pytest.mark.gpu
