@@ -1,6 +1,7 @@
 """In-process A/B of two libqhuff.so builds: one process, one set of device
 buffers, the two libraries' kernels timed alternately (blocks of launches,
-HIP events per launch on the launch stream), so box-to-box and
+each launch timed by its own dispatch timestamps (qhuff_timing_*, ABI 4;
+HIP events per launch for older libraries), so box-to-box and
 process-to-process variance cancel.  Prints per-library median and mean
 kernel times for encode and decode of the bench workload (1,048,576 token
 strings, 8-64 B).
@@ -28,6 +29,12 @@ def load(path):
     L.qhuff_decode_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp, vp]
     ctx = C.c_void_p()
     assert L.qhuff_open(0, C.byref(ctx)) == 0
+    try:
+        L.qhuff_timing_enable.argtypes = [vp, C.c_int]
+        L.qhuff_timing_read.argtypes = [vp, vp, vp, C.c_uint32]
+        L.timed = True
+    except AttributeError:
+        L.timed = False
     return L, ctx
 
 
@@ -80,6 +87,17 @@ def main():
     for r in range(rounds):
         for k in ((0, 1) if r % 2 == 0 else (1, 0)):
             for op, fn in (("enc", enc), ("dec", dec)):
+                lb, ctx = L[k]
+                if lb.timed:
+                    lb.qhuff_timing_enable(ctx, 1)
+                    for i in range(per):
+                        fn(k)
+                    kinds = (C.c_uint32 * per)()
+                    us = (C.c_double * per)()
+                    m = lb.qhuff_timing_read(ctx, kinds, us, per)
+                    lb.qhuff_timing_enable(ctx, 0)
+                    times[(k, op)] += [us[i] for i in range(m)]
+                    continue
                 ev = [torch.cuda.Event(enable_timing=True)
                       for _ in range(per + 1)]
                 ev[0].record(stream)
