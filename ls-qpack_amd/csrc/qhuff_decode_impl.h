@@ -453,6 +453,301 @@ write_bytes(QH_LDS uint8_t *d, uint32_t v, uint32_t nb)
         d[2] = (uint8_t) (v >> 16);
 }
 
+// ---- long strings: wave-cooperative decode ----
+//
+// One lane walks one string: a tile's time is its longest string's.  On the
+// reference's own header corpora (tests/golden/data/*.qif) a tile's longest
+// string is ~13x its mean one (cookies, user agents, 1,461-byte values), so
+// the lanes idle.  A string of more than kCoopMin Huffman bytes is decoded
+// by the whole wave instead, its bits cut into segments of S bits (a
+// multiple of 32, >= kSegMin, at most 64 segments), one per lane:
+//   A  every lane walks its segment from the segment's first bit -- a guess:
+//      only lane 0 starts on a code boundary -- and marks the bit of each
+//      symbol start it passes in a bitmap (one bit per input bit);
+//   B  lane j then walks on from its exit -- the first symbol start past its
+//      segment -- into segment j + 1 until it reaches a marked bit: from
+//      there on its walk and lane j + 1's are the same walk (decoding is a
+//      function of the position), so lane j + 1's exit is exact if lane j's
+//      was.  Lane 0's is; a lane whose predecessor's walk crossed its whole
+//      segment without meeting its marks takes that walk's exit instead and
+//      walks on again (rare; at most one round per segment).  Huffman codes
+//      resynchronise after a median of ~31 bits on that corpus
+//      (90th percentile ~160), so B costs a fraction of A;
+//   then the symbols of segment j are the ones B counted before the meeting
+//   point plus lane j's marks after it; a wave scan gives each segment's
+//   output offset, and
+//   W  every lane decodes its segment again from its now exact first symbol
+//      start, into the string's arena slot at that offset, with the D3 checks.
+// A string whose W finds an error (EOS code, bad padding), or whose counts
+// or exits disagree, is decoded again by its own lane (decode_string_lds),
+// so the result is always the one-lane result.  Cost: ~3 walks of S bits
+// per string against one walk of the whole string.
+#ifndef QH_COOP_MIN
+#define QH_COOP_MIN 128
+#endif
+constexpr uint32_t kCoopMin = QH_COOP_MIN;      // Huffman bytes
+#ifndef QH_SEG_MIN
+#define QH_SEG_MIN 128
+#endif
+constexpr uint32_t kSegMin = QH_SEG_MIN;        // bits per segment
+static_assert(kSegMin % 32 == 0 && kSegMin >= 64, "segment bits");
+constexpr uint32_t kCoopDummy = 64;             // per-lane sink bytes
+
+enum WalkMode { kWalkMark, kWalkCheck, kWalkEmit };
+
+// Walk the symbols of the staged stream src that start at [pos, lim) of the
+// string ending at bitend (lim <= bitend; a walk that reaches the string's
+// last < kWinBits bits decodes them padded, as decode_string_lds), one or
+// two symbols a step; pos ends on the first symbol start >= lim (or where
+// the walk stopped).  n counts the symbols.  Mark: set each symbol start's
+// bit in bm (bit x - b0).  Check: stop on a symbol start whose bit is set
+// (hit = 1).  Emit: store the symbols at dst, below dend (the bytes a step
+// does not emit, or past dend, go to the lane's sink byte), hit = 1 on an
+// error (D3).  A code the string
+// cannot hold (EOS, or running past bitend) ends the walk there.
+template <int Mode>
+__device__ __forceinline__ void
+seg_walk(const QH_LDS uint32_t *src, uint32_t &pos, uint32_t lim,
+         uint32_t bitend, const QH_LDS uint32_t *s_win,
+         const QH_LDS uint16_t *s_sorted, QH_LDS uint32_t *bm, uint32_t b0,
+         QH_LDS uint8_t *dst, QH_LDS uint8_t *dend, QH_LDS uint8_t *sink,
+         uint32_t &n, uint32_t &hit)
+{
+    uint32_t A, B, t, p, nx;
+    {
+        const uint32_t i0 = pos >> 5, sk = pos & 31;
+        A = src[i0];
+        const uint32_t a1 = src[i0 + 1];
+        B = sk ? a1 : A;
+        t = (32 - sk) & 31;
+        p = sk ? i0 + 2 : i0 + 1;
+        nx = src[p];
+    }
+    auto advance = [&](uint32_t c) {
+        uint32_t tn;
+        const bool cross = __builtin_sub_overflow(t, c, &tn);
+        A = cross ? B : A;
+        B = cross ? nx : B;
+        t = tn & 31;
+        p += cross ? 1u : 0u;
+        nx = src[p];
+    };
+    auto marked = [&](uint32_t x, bool live) -> bool {
+        const uint32_t r = x - b0;
+        const uint32_t w = bm[live ? r >> 5 : 0u];
+        return live & (((w >> (r & 31)) & 1u) != 0);
+    };
+    auto hook = [&](uint32_t e, uint32_t nb, uint32_t l0) {
+        if constexpr (Mode == kWalkMark)
+        {
+            const uint32_t r0 = pos - b0, r1 = r0 + l0;
+            if (nb >= 1)
+                __hip_atomic_fetch_or(&bm[r0 >> 5], 1u << (r0 & 31),
+                                      __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (nb == 2)
+                __hip_atomic_fetch_or(&bm[r1 >> 5], 1u << (r1 & 31),
+                                      __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        else if constexpr (Mode == kWalkEmit)
+        {
+            QH_LDS uint8_t *a0 = ((nb >= 1) & (dst < dend)) ? dst : sink;
+            QH_LDS uint8_t *a1 = ((nb == 2) & (dst + 1 < dend)) ? dst + 1 : sink;
+            *a0 = (uint8_t) e;
+            *a1 = (uint8_t) (e >> 16);
+            dst += nb;
+        }
+        n += nb;
+    };
+    constexpr uint32_t kMain = kWinBits;
+    uint32_t W = __builtin_amdgcn_alignbit(A, B, t);
+    for (;;)
+    {
+        bool live;
+        uint32_t e;
+        do
+        {
+            live = (pos < lim) & (bitend - pos >= kMain);
+            const uint32_t idx =
+                ((W >> (32 - kWinBits - 2)) & (live ? 4u * (kWinSize - 1) : 0u))
+                | (live ? 0u : 4u * kHoldIdx);
+            e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
+            if constexpr (Mode == kWalkCheck)
+            {
+                const bool m = marked(pos, live);
+                hit |= m ? 1u : 0u;
+                lim = m ? pos : lim;
+                e = m ? kHoldEntry : e;
+            }
+            const uint32_t ns = ent_ns(e), l0 = ent_l0(e);
+            const bool cut = (ns == 2) & (pos + l0 >= lim);
+            const uint32_t nb = cut ? 1u : ns;
+            const uint32_t c = cut ? l0 : ent_c(e);
+            hook(e, nb, l0);
+            pos += c;
+            advance(c);
+            W = __builtin_amdgcn_alignbit(A, B, t);
+        } while (__builtin_amdgcn_ballot_w64(live & (e >= (1u << 24))));
+        // lanes stalled on a code of 14..30 bits
+        const bool lng = (pos < lim) & (bitend - pos >= kMain);
+        if (__builtin_expect(!__builtin_amdgcn_ballot_w64(lng), 1))
+            break;
+        uint32_t L;
+        const uint32_t sym = long_code(W, s_sorted, &L);
+        const bool rej = lng & ((sym == 256) | (L > bitend - pos));
+        const bool ok = lng & !rej;
+        if constexpr (Mode == kWalkEmit)
+            hit |= rej ? 1u : 0u;
+        lim = rej ? pos : lim;
+        hook(sym, ok ? 1u : 0u, 0u);
+        const uint32_t c = ok ? L : 0u;
+        pos += c;
+        advance(c);
+        W = __builtin_amdgcn_alignbit(A, B, t);
+    }
+    // the string's last < kWinBits bits: at most two symbols, then padding
+    {
+        const uint32_t rem = bitend - pos;
+        bool live = (pos < lim) & (rem < kMain);
+        if constexpr (Mode == kWalkCheck)
+        {
+            const bool m = marked(pos, live);
+            hit |= m ? 1u : 0u;
+            live = live & !m;
+        }
+        const uint32_t w = W | (0xffffffffu >> (rem & 31));
+        const uint32_t e = s_win[w >> (32 - kWinBits)];
+        const uint32_t ns = ent_ns(e), ct = ent_c(e), l0 = ent_l0(e);
+        const bool two = (ns == 2) & (ct <= rem);
+        const bool one = !two & (ns != 0) & (l0 <= rem);
+        const uint32_t c = live ? (two ? ct : (one ? l0 : 0u)) : 0u;
+        hook(e, live ? (two ? 2u : (one ? 1u : 0u)) : 0u, l0);
+        if constexpr (Mode == kWalkEmit)
+        {
+            const uint32_t r2 = rem - c;             // padding bits
+            const uint32_t inv = ~(w << (c & 31));
+            const bool pad_ok = r2 < 8
+                             && (r2 == 0 || (inv >> ((32 - r2) & 31)) == 0);
+            hit |= (live & !pad_ok) ? 1u : 0u;
+        }
+        pos += c;
+    }
+}
+
+// popcount of the bits [r0, r1) of bm, every lane its own range (r1 <= r0
+// for an empty one); no lane branches past the trip count
+__device__ __forceinline__ uint32_t
+bm_count(const QH_LDS uint32_t *bm, uint32_t r0, uint32_t r1)
+{
+    const uint32_t w0 = r0 >> 5;
+    const uint32_t w1 = r1 > r0 ? (r1 + 31) >> 5 : w0;
+    const uint32_t K = wave_max_dpp(w1 - w0);
+    uint32_t c = 0;
+    for (uint32_t k = 0; k < K; ++k)
+    {
+        const uint32_t w = w0 + k;
+        uint32_t v = w < w1 ? bm[w] : 0u;
+        v = k == 0 ? v >> (r0 & 31) : v;
+        c += __builtin_popcount(v);
+    }
+    return c;
+}
+
+// Decode the string at bits [b0, b1) of the stage with the whole wave, into
+// the arena bytes at `slot` (every lane gets the result).  bm: a zeroed-on-
+// entry bitmap of (b1 - b0) / 32 + 2 words; sink: kCoopDummy bytes.
+// Returns the output length, or -1 when the one-lane decode must do it (an
+// invalid string, or any disagreement).
+__device__ __forceinline__ int
+coop_decode(const QH_LDS uint32_t *src, uint32_t b0, uint32_t b1,
+            QH_LDS uint8_t *slot, QH_LDS uint32_t *bm, QH_LDS uint8_t *sink,
+            const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t nbits = b1 - b0;
+    uint32_t S = (((nbits + 63) >> 6) + 31) & ~31u;
+    S = S > kSegMin ? S : kSegMin;
+    const uint32_t nseg = nbits / S > 0 ? nbits / S : 1u;   // <= 64
+    const bool act = lane < nseg;
+    const uint32_t s = act ? b0 + lane * S : b1;
+    const uint32_t stop = lane + 1 < nseg ? s + S : b1;
+    const uint32_t nw = nbits / 32 + 2;
+    for (uint32_t i = lane; i < nw; i += 64)
+        bm[i] = 0;
+    wave_sync();
+    // A: guessed walks, marking
+    uint32_t E = s, C = 0, h = 0;
+    seg_walk<kWalkMark>(src, E, stop, b1, s_win, s_sorted, bm, b0, nullptr,
+                        nullptr, sink, C, h);
+    wave_sync();
+    // B: walk on into the next segment until meeting its marks
+    const bool cl = act & (lane + 1 < nseg);
+    const uint32_t lim2 = !cl ? b1 : lane + 2 < nseg ? s + 2 * S : b1;
+    uint32_t cs = E, X = 0, K = 0, met = 0;
+    bool redo = cl;
+    uint32_t pm = 0, px = 0, rounds = 0;
+    while (__builtin_amdgcn_ballot_w64(redo))
+    {
+        uint32_t x = redo ? cs : b1, k = 0, hm = 0;
+        seg_walk<kWalkCheck>(src, x, redo ? lim2 : b1, b1, s_win, s_sorted, bm,
+                             b0, nullptr, nullptr, sink, k, hm);
+        X = redo ? x : X;
+        K = redo ? k : K;
+        met = redo ? hm : met;
+        // lane j >= 1: its exact exit is its own (lane j - 1 met its walk)
+        // or lane j - 1's walk's
+        pm = wave_shr1(met);
+        px = wave_shr1(X);
+        const uint32_t tE = (lane >= 1 && !pm) ? px : E;
+        redo = cl & (tE != cs);
+        cs = cl ? tE : cs;
+        if (++rounds > 64)                   // (cannot happen: a lane's exit
+            return -1;                       // is fixed after j rounds)
+    }
+    // symbols of each segment
+    const uint32_t kp = wave_shr1(K);
+    const uint32_t own = bm_count(bm, (act && lane >= 1 && pm) ? px - b0 : 0u,
+                                  (act && lane >= 1 && pm) ? stop - b0 : 0u);
+    const uint32_t T = !act ? 0u : lane == 0 ? C : kp + own;
+    const uint32_t incl = wave_incl_scan(T);
+    const uint32_t N = read_lane(incl, 63);
+    if (N > (8 * (nbits >> 3)) / 5)          // more than the slot holds
+        return -1;
+    // W: decode from the exact first symbol starts
+    const uint32_t ts = lane == 0 ? b0 : wave_shr1(cs);
+    uint32_t x = act ? ts : b1, m = 0, bad = 0;
+    seg_walk<kWalkEmit>(src, x, act ? stop : b1, b1, s_win, s_sorted, bm, b0,
+                        slot + (incl - T), slot + N, sink + lane, m, bad);
+    // each exit must be the next segment's start; the last one the end
+    const uint32_t nts = (uint32_t) __shfl_down((int) ts, 1, 64);
+    const bool chain = !act || (lane + 1 < nseg ? x == nts : true);
+    if (__builtin_amdgcn_ballot_w64(act & ((m != T) | (bad != 0) | !chain)))
+        return -1;
+    return (int) N;
+}
+
+// copy n bytes src -> dst (LDS) with the whole wave: whole dwords at dst,
+// the unaligned head and tail bytewise
+__device__ __forceinline__ void
+copy_wave(const QH_LDS uint8_t *src, QH_LDS uint8_t *dst, uint32_t n)
+{
+    const uint32_t lane = lane_id();
+    uint32_t h = (4 - ((uint32_t) (uintptr_t) dst & 3)) & 3;
+    h = h < n ? h : n;
+    const uint32_t nb = (n - h) >> 2;
+    const uint32_t it = h + 4 * nb;
+    const uint32_t sb = (uint32_t) (uintptr_t) (src + h), r = sb & 3;
+    const QH_LDS uint32_t *sw = (const QH_LDS uint32_t *) (src + h - r);
+    QH_LDS uint32_t *dw = (QH_LDS uint32_t *) (dst + h);
+    for (uint32_t i = lane; i < nb; i += 64)
+        dw[i] = align_bytes(sw[i + 1], sw[i], r);
+    if (lane < h)
+        dst[lane] = src[lane];
+    if (lane >= 4 && lane - 4 < n - it)
+        dst[it + lane - 4] = src[it + lane - 4];
+}
+
 // Arena slot -> stage at byte D, for every lane of the wave at once, with
 // whole dwords and no per-dword lane branches (the per-lane copy it replaced,
 // with one lane branch per dword, is neutral-to-slower: profiles/r03_robust): each lane's body dwords go out in trips of
@@ -585,6 +880,7 @@ struct DecPolicyT
     QH_LDS SM *sm;
     QH_LDS DecWave *wv;
     uint32_t slot0;                  // this lane's arena slot (current tile)
+    uint64_t coop = 0;               // strings decoded by the whole wave
 
     __device__ __forceinline__ void stage_in(const Chunks<kNch> &ch,
                                              const Span &sp, const Offs &)
@@ -596,36 +892,95 @@ struct DecPolicyT
     {
         return wv->in;
     }
-    // staged tile: decode this lane's string into its arena slot
+    // staged tile: decode this lane's string into its arena slot; strings
+    // above kCoopMin Huffman bytes with the whole wave (coop_decode), when
+    // their bitmap fits in the arena past the slots
     __device__ __forceinline__ void codec(const Offs &to, uint32_t cnt,
                                           const Span &sp, uint32_t *sz,
                                           uint32_t *st)
     {
         const uint32_t lane = lane_id();
         const uint32_t A = to.first();
+        const uint32_t hl = to.o1 - to.o0;
         const bool fixed = !__builtin_amdgcn_ballot_w64(
-            (lane < cnt) & (to.o1 - to.o0 > kFixMaxLen));
+            (lane < cnt) & (hl > kFixMaxLen));
         slot0 = fixed ? kFixStride * lane
                       : 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
+        const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
+        const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
+        // the slots end below kVarArenaBytes - slack + 1 for this span; the
+        // bitmap (hl / 4 + 2 words) and the sinks go above them
+        const uint32_t slots_end = 2 * kDecTS
+                                 + (uint32_t) ((8ull * (to.last() - A)) / 5) + 2;
+        const bool lng = !fixed && (lane < cnt) && hl > kCoopMin
+                      && slots_end + 4 * (hl / 4 + 2) + kCoopDummy
+                             <= (uint32_t) kArenaBytes;
+        coop = __builtin_amdgcn_ballot_w64(lng);
         int r = 0;
         if (lane < cnt)
         {
-            const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
-            const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
             ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
-            r = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted,
-                                  em);
+            r = decode_string_lds(wv->in, 8 * rs, lng ? 8 * rs : 8 * re,
+                                  sm->win, sm->sorted, em);
+        }
+        if (coop)
+        {
+            QH_LDS uint8_t *sink = wv->arena + kArenaBytes - kCoopDummy;
+            uint64_t m = coop, fail = 0;
+            while (m)
+            {
+                const uint32_t j = (uint32_t) __builtin_ctzll(m);
+                m &= m - 1;
+                const uint32_t b0 = 8 * read_lane(rs, j);
+                const uint32_t b1 = 8 * read_lane(re, j);
+                const uint32_t nw = (b1 - b0) / 32 + 2;
+                QH_LDS uint32_t *bm =
+                    (QH_LDS uint32_t *) (sink - 4 * nw);
+                const int rc = coop_decode(wv->in, b0, b1,
+                                           wv->arena + read_lane(slot0, j), bm,
+                                           sink, sm->win, sm->sorted);
+                if (rc < 0)
+                    fail |= 1ull << j;
+                else
+                    r = lane == j ? rc : r;
+            }
+            if (fail)
+            {
+                // (rare) an invalid string: its own lane decodes it again
+                coop &= ~fail;
+                const bool f = (fail >> lane) & 1;
+                ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
+                const int r2 = decode_string_lds(wv->in, 8 * rs,
+                                                 f ? 8 * re : 8 * rs, sm->win,
+                                                 sm->sorted, em);
+                r = f ? r2 : r;
+            }
         }
         *sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
         *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
     }
-    // arena -> the (dead) input stage, compacted
+    // arena -> the (dead) input stage, compacted (the cooperative strings
+    // by the whole wave, after the rest)
     __device__ __forceinline__ void emit(uint32_t excl, uint32_t sz, uint32_t)
     {
 #ifdef QH_TIME_NO_EMIT                       // timing builds only: no output
         return;
 #endif
-        compact_wave(wv->arena + slot0, (QH_LDS uint8_t *) wv->in + excl, sz);
+        QH_LDS uint8_t *stage = (QH_LDS uint8_t *) wv->in;
+        compact_wave(wv->arena + slot0, stage + excl,
+                     (coop >> lane_id()) & 1 ? 0u : sz);
+        if (coop)
+        {
+            wave_sync();
+            uint64_t m = coop;
+            while (m)
+            {
+                const uint32_t j = (uint32_t) __builtin_ctzll(m);
+                m &= m - 1;
+                copy_wave(wv->arena + read_lane(slot0, j),
+                          stage + read_lane(excl, j), read_lane(sz, j));
+            }
+        }
     }
 
     // a tile of the batch kernel: base from the look-back

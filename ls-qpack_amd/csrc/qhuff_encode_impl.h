@@ -19,6 +19,15 @@
 #define QH_ENC_DEPTH 3
 #endif
 
+// the dense pass's code table in 32 copies, copy c on LDS bank c, lane l
+// reading copy l % 32 (dense_pass): the 64 lookups of a wave are bank-
+// conflict-free (one copy: text bytes hit a few dozen entries of a 1 KB
+// table, several to a bank).  32 KB of LDS, which the batch kernel has
+// free; the service kernel keeps one copy.
+#ifndef QH_MT_REP
+#define QH_MT_REP 1
+#endif
+
 namespace qhuff {
 
 constexpr int kEncInCap = kStageCap;          // staged input bytes per tile
@@ -39,9 +48,10 @@ struct EncWave                                // one wave's private LDS region
 
 struct EncSmem
 {
+    static constexpr bool kMtRep = QH_MT_REP;
     u32x2 enc[257];
-    uint32_t mt[256];                // dense pass: code | len << 27 (len <= 15),
-                                     // 31 << 27 for longer codes
+    uint32_t mt[256];                // dense pass: code[26:0] | len << 27
+    uint32_t mtr[kMtRep ? 256 * 32 : 1];   // mt, 32 copies: [byte][copy]
     uint8_t len[256];
     EncWave w[kWaves];
     BlockTickets tk;                 // the workgroup's first tickets
@@ -442,9 +452,11 @@ dense_or(QH_LDS uint32_t *dense, uint32_t pos, uint32_t v, uint32_t len)
 // l, l + 64, l + 128): code lengths per byte (u8, into the out stage), the
 // dense offset of every chunk (s0) and the codes of all span bytes back to
 // back in `dense` -- the bytes around the tile's strings included (their
-// codes shift every offset by the same amount).  Returns whether the dense
-// stream is usable: every code of the span at most 15 bits.
-__device__ __forceinline__ bool
+// codes shift every offset by the same amount).  Codes of any length (a
+// stream longer than `dense` is caught by the codec's size check: its ORs
+// pile up on the last two words).
+template <bool Rep>
+__device__ __forceinline__ void
 dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
 {
     const uint32_t lane = lane_id();
@@ -453,7 +465,7 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
         d4[i] = (u32x4){0, 0, 0, 0};
     wave_sync();
     QH_LDS u32x4 *lens4 = (QH_LDS u32x4 *) wv->out;
-    uint32_t carry = 0, big = 0;
+    uint32_t carry = 0;
     // (the three rows' stage chunks read up front, one LDS round trip: enc
     // 66.1 vs 65.4 us, profiles/r02_l/ab_rows_first.txt)
 #pragma unroll
@@ -467,9 +479,20 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
         const u32x4 w = ((const QH_LDS u32x4 *) wv->in)[c < last ? c : last];
         const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
         uint32_t m[16];
+        // (Rep) this lane's copy, rebuilt per row by an opaque instruction:
+        // left to itself the compiler keeps it live through the tile loop,
+        // and at 168 VGPRs that spills the sizing phase's offsets
+        uint32_t copy = 0;
+        if (Rep)
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\t"
+                         "v_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
+                         "v_and_b32 %0, 31, %0" : "=v"(copy));
 #pragma unroll
         for (int j = 0; j < 16; ++j)
-            m[j] = mt[(wd[j >> 2] >> (8 * (j & 3))) & 0xffu];
+        {
+            const uint32_t b = (wd[j >> 2] >> (8 * (j & 3))) & 0xffu;
+            m[j] = mt[Rep ? (b << 5) | copy : b];
+        }
         uint32_t lp[4], G[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g)
@@ -478,7 +501,6 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
                   | ((m[4 * g + 2] >> 27) << 16) | ((m[4 * g + 3] >> 27) << 24);
             G[g] = __builtin_amdgcn_sad_u8(lp[g], 0u, 0u);
         }
-        big |= (lp[0] | lp[1] | lp[2] | lp[3]) & 0x10101010u;
         const uint32_t T = G[0] + G[1] + G[2] + G[3];
         const uint32_t incl = wave_incl_scan(T);
         const uint32_t p0 = carry + incl - T;
@@ -499,10 +521,29 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
             }
             if (__builtin_amdgcn_ballot_w64(G[g] > 32))
             {
-                // a lane's four codes exceed 32 bits: two pairs of <= 30
-                dense_or(wv->dense, pos, (cd[0] << L[1]) | cd[1], L[0] + L[1]);
-                dense_or(wv->dense, pos + L[0] + L[1], (cd[2] << L[3]) | cd[3],
-                         L[2] + L[3]);
+                // (rare) a code of 28 or 30 bits: its ones above bit 26
+                if (__builtin_amdgcn_ballot_w64(((lp[g] + 0x64646464u)
+                                                 & 0x80808080u) != 0))
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        cd[j] |= L[j] > 27 ? (0xffffffffu >> (32 - L[j]))
+                                                 & ~0x7ffffffu
+                                           : 0u;
+                const uint32_t a = L[0] + L[1], b = L[2] + L[3];
+                if (__builtin_amdgcn_ballot_w64((a > 32) | (b > 32)))
+                {
+                    // (rare) codes above 16 bits: one OR per code
+                    dense_or(wv->dense, pos, cd[0], L[0]);
+                    dense_or(wv->dense, pos + L[0], cd[1], L[1]);
+                    dense_or(wv->dense, pos + a, cd[2], L[2]);
+                    dense_or(wv->dense, pos + a + L[2], cd[3], L[3]);
+                }
+                else
+                {
+                    // a lane's four codes exceed 32 bits: two pairs
+                    dense_or(wv->dense, pos, (cd[0] << L[1]) | cd[1], a);
+                    dense_or(wv->dense, pos + a, (cd[2] << L[3]) | cd[3], b);
+                }
             }
             else
             {
@@ -514,7 +555,6 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
             pos += G[g];
         }
     }
-    return !__builtin_amdgcn_ballot_w64(big != 0);
 }
 
 // dense offset of span byte p (p <= 16 * n16): the offset of the chunk
@@ -541,6 +581,7 @@ dense_at(const QH_LDS EncWave *wv, uint32_t p)
 // stage (byte order): one 32-bit window of the dense stream per output word;
 // plain stores for the words the string owns whole, OR for its first and
 // last word (shared with framing, padding and the neighbours)
+template <bool Mid = true>
 __device__ __forceinline__ void
 copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
            QH_LDS uint32_t *st, uint32_t d)
@@ -578,7 +619,8 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
     if (wl == w0)
         return;
     QH_LDS uint32_t *o = st + w0 + 1;
-    for (uint32_t k = 0; k < nmid; k += 4)
+    // (!Mid: the whole wave copies the middle words, copy_dense_mid)
+    for (uint32_t k = 0; k < (Mid ? nmid : 0u); k += 4)
     {
         if (k)
         {
@@ -600,9 +642,35 @@ copy_dense(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// one string from the dense stream: framing, payload bits [s, s + bits),
-// padding; raw strings (E3 fallback) from the staged input
+// the words a string of nb dense bits from bit s to the byte-aligned bit d
+// owns whole (copy_dense<false> leaves them), by the whole wave
 __device__ __forceinline__ void
+copy_dense_mid(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
+               QH_LDS uint32_t *st, uint32_t d)
+{
+    const uint32_t w0 = d >> 5, wl = (d + nb - 1) >> 5;
+    const uint32_t nmid = wl > w0 ? wl - w0 - 1 : 0u;
+    const uint32_t x1 = s - (d & 31) + 32, sh = x1 & 31, q = x1 >> 5;
+    QH_LDS uint32_t *o = st + w0 + 1;
+    for (uint32_t k = lane_id(); k < nmid; k += 64)
+    {
+        const uint32_t a = dense[q + k], b = dense[q + k + 1];
+        o[k] = bswap32(sh ? __builtin_amdgcn_alignbit(a, b, 32 - sh) : a);
+    }
+}
+
+// Huffman payloads of more dense bits than this are copied by the whole
+// wave (a lane alone copies 4 words a trip: a 1 KB value would take ~60
+// trips while the others idle)
+#ifndef QH_ENC_COOP_BITS
+#define QH_ENC_COOP_BITS 1024
+#endif
+constexpr uint32_t kEncCoopBits = QH_ENC_COOP_BITS;
+
+// one string from the dense stream: framing, payload bits [s, s + bits),
+// padding; raw strings (E3 fallback) from the staged input.  Returns the
+// payload's first bit.
+__device__ __forceinline__ uint32_t
 emit_dense(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
            const EncSize &z, const QH_LDS uint32_t *dense, uint32_t s,
            uint32_t bits, const QH_LDS u32x2 *s_enc, QH_LDS uint32_t *st,
@@ -611,10 +679,11 @@ emit_dense(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
     uint32_t pos = 8 * start;
     if (mode)
         pos = emit_prefix(st, pos, mode, z.huff, z.plen);
+    const uint32_t p0 = pos;
     if (!z.huff)
     {
         pack_bits(in, rs, re, true, s_enc, st, pos);
-        return;
+        return p0;
     }
     if (bits)
     {
@@ -624,6 +693,7 @@ emit_dense(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
         if (pad)
             or_bits(st, pos, (1u << pad) - 1, pad);
     }
+    return p0;
 }
 
 // A tile whose input or output does not fit the stages, coded eagerly:
@@ -704,7 +774,11 @@ struct EncPolicyT
     // have been issued into the chunk registers)
     __device__ __forceinline__ void prepare(const Span &sp)
     {
-        dense = dense_pass(sp.n16, sm->mt, wv);
+        if constexpr (SM::kMtRep)
+            dense_pass<true>(sp.n16, sm->mtr, wv);
+        else
+            dense_pass<false>(sp.n16, sm->mt, wv);
+        dense = true;
     }
     __device__ __forceinline__ const QH_LDS uint32_t *out_stage() const
     {
@@ -749,15 +823,40 @@ struct EncPolicyT
 #ifdef QH_TIME_NO_EMIT                       // timing builds only: no output
         return;
 #endif
-        if (sz)
+        if (dense)
         {
-            if (dense)
-                emit_dense(wv->in, rs, re, mode, z, wv->dense, ds, bits,
-                           sm->enc, wv->out, excl);
-            else
-                emit_bits(wv->in, rs, re, mode, z.huff, z.plen, sm->enc,
-                          wv->out, excl);
+            // long payloads: their middle words by the whole wave, after
+            const bool lc = (sz != 0) & z.huff & (bits > kEncCoopBits);
+            const uint64_t lm = __builtin_amdgcn_ballot_w64(lc);
+            uint32_t p0 = 0;
+            if (sz)
+                p0 = emit_dense(wv->in, rs, re, mode, z, wv->dense, ds,
+                                lc ? 0u : bits, sm->enc, wv->out, excl);
+            if (lm)
+            {
+                if (lc)
+                {
+                    // its first and last words (shared), and the padding
+                    copy_dense<false>(wv->dense, ds, bits, wv->out, p0);
+                    const uint32_t pe = p0 + bits;
+                    const uint32_t pad = (8 - (pe & 7)) & 7;
+                    if (pad)
+                        or_bits(wv->out, pe, (1u << pad) - 1, pad);
+                }
+                uint64_t m = lm;
+                while (m)
+                {
+                    const uint32_t j = (uint32_t) __builtin_ctzll(m);
+                    m &= m - 1;
+                    copy_dense_mid(wv->dense, read_lane(ds, j),
+                                   read_lane(bits, j), wv->out,
+                                   read_lane(p0, j));
+                }
+            }
         }
+        else if (sz)
+            emit_bits(wv->in, rs, re, mode, z.huff, z.plen, sm->enc, wv->out,
+                      excl);
     }
 
     // a tile of the batch kernel: base from the look-back
@@ -798,7 +897,17 @@ enc_tables_load(QH_LDS SM *sm, const uint2 *enc_g, int tid)
         if (tid < 256)
         {
             sm->len[tid] = (uint8_t) e.y;
-            sm->mt[tid] = e.y <= 15 ? (e.x | (e.y << 27)) : (31u << 27);
+            // (codes of 28 and 30 bits keep their low 27: the bits above
+            // are ones, dense_pass puts them back)
+            const uint32_t m = (e.x & 0x7ffffffu) | (e.y << 27);
+            sm->mt[tid] = m;
+            if constexpr (SM::kMtRep)
+            {
+                QH_LDS u32x4 *r = (QH_LDS u32x4 *) &sm->mtr[tid * 32];
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    r[k] = (u32x4){m, m, m, m};
+            }
         }
     }
 }

@@ -38,6 +38,7 @@ union SvcWave
 
 struct SvcSmem
 {
+    static constexpr bool kMtRep = false;   // (no LDS left for 32 copies)
     uint32_t win[kWinSize + 4];      // decode window table + the hold entry
     uint16_t sorted[257];
     u32x2 enc[257];                  // encode tables (enc_tables_load)

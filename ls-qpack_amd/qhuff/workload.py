@@ -11,9 +11,13 @@
   kernels, by the kernels' own rules (host arithmetic over the offsets; no
   device needed): slow tiles (input span or output past the 3 KB stages,
   qhuff_pipeline.h / qhuff_decode_impl.h), decode tiles whose arena slots are
-  placed by input offset (a string above kFixMaxLen Huffman bytes), encode
-  tiles that fall back from the dense stream to per-string packing (a code
-  above 15 bits in the span, qhuff_encode_impl.h dense_pass).
+  placed by input offset (a string above kFixMaxLen Huffman bytes), decode
+  tiles with a string the whole wave decodes (above kCoopMin Huffman bytes,
+  its bitmap fitting past the arena slots: qhuff_decode_impl.h
+  coop_decode), encode tiles that fall back from the dense stream to
+  per-string packing (the span's codes overflow the dense stream,
+  qhuff_encode_impl.h dense_pass) and encode tiles with a payload the whole
+  wave copies (above kEncCoopBits dense bits).
 """
 import os
 
@@ -46,11 +50,16 @@ QIF_NAMES = ("fb-req.qif", "fb-resp.qif", "long-codes.qif", "netbsd.qif")
 LONG_CODE_BYTES = bytes([1, 2, 6, 92, 141])
 
 # kernel constants the shares follow (qhuff_pipeline.h kStageCap,
-# qhuff_decode_impl.h kFixMaxLen, qhuff_encode_impl.h kDenseBits)
+# qhuff_decode_impl.h kFixMaxLen / kArenaBytes / kCoopMin / kCoopDummy,
+# qhuff_encode_impl.h kDenseBits / kEncCoopBits)
 STAGE = 3072
 TILE = 64
 FIX_MAX_LEN = (5 * (108 - 1)) // 8
+ARENA = 64 * 108
+COOP_MIN = 128
+COOP_DUMMY = 64
 DENSE_BITS = 32 * (STAGE // 4 + 4 - 2)
+ENC_COOP_BITS = 1024
 
 
 def qif_strings(paths):
@@ -118,6 +127,13 @@ def tile_shares(data, off, hoff):
     hl = np.diff(hoff)
     max_hl = np.maximum.reduceat(hl, t0) if len(hl) else np.zeros(nt, np.int64)
     var_arena = dec_fast & (max_hl > FIX_MAX_LEN)
+    # a cooperative string: above COOP_MIN, its bitmap past the slots
+    slots_end = 2 * TILE + (8 * (b - a)) // 5 + 2
+    coop_ok = (hl > COOP_MIN) & (np.repeat(slots_end, t1 - t0)
+                                 + 4 * (hl // 4 + 2) + COOP_DUMMY <= ARENA)
+    any_coop = (np.maximum.reduceat(coop_ok.astype(np.int64), t0) > 0
+                if len(hl) else np.zeros(nt, bool))
+    coop = var_arena & any_coop
     # ---- encode tiles (payload mode) ----
     ea, eb = off[t0], off[t1]
     epa, epb = _span(ea, eb)
@@ -126,11 +142,12 @@ def tile_shares(data, off, hoff):
     enc_fast = enc_staged & (enc_total + 64 <= STAGE)
     lens = RFC_LEN[data.astype(np.int64)] if len(data) else np.zeros(0, np.int64)
     plen = np.concatenate([[0], np.cumsum(lens)])
-    plong = np.concatenate([[0], np.cumsum(lens > 15)])
-    epb_c = np.minimum(epb, len(data))
-    long_in_span = plong[epb_c] - plong[epa] > 0
     dense_bits = plen[eb] - plen[epa]
-    dense = enc_fast & ~long_in_span & (dense_bits + 64 <= DENSE_BITS)
+    dense = enc_fast & (dense_bits + 64 <= DENSE_BITS)
+    sbits = plen[off[1:]] - plen[off[:-1]]
+    big = (np.maximum.reduceat(sbits, t0) if len(sbits)
+           else np.zeros(nt, np.int64))
+    enc_coop = dense & (big > ENC_COOP_BITS)
     f = lambda m: round(float(m.mean()), 4) if nt else 0.0
     hist = np.percentile(np.diff(off), [50, 90, 99, 100]) if len(off) > 1 \
         else [0, 0, 0, 0]
@@ -138,7 +155,9 @@ def tile_shares(data, off, hoff):
         "tiles": int(nt),
         "decode_slow_tile_share": f(~dec_fast),
         "decode_var_arena_share": f(var_arena),
+        "decode_coop_tile_share": f(coop),
         "encode_slow_tile_share": f(~enc_fast),
         "encode_fallback_share": f(enc_fast & ~dense),
+        "encode_coop_tile_share": f(enc_coop),
         "raw_len_p50_p90_p99_max": [int(x) for x in hist],
     }

@@ -274,6 +274,68 @@ def test_edge_batches(codec):
     check_decode(codec, h, ho)
 
 
+def _long_tiles(rng, n_tiles, lens, alpha, corrupt=None):
+    """Tiles of one long Huffman string (raw length from lens) among 63
+    short ones (qhuff_decode_impl.h coop_decode); corrupt(i, h) may alter
+    the long string's encoding."""
+    strs = []
+    for t in range(n_tiles):
+        short = [O.huffman_enc(s) for s in
+                 rand_strings(rng, 63, ALPHAS["token"], 0, 24)]
+        s = bytes(rng.choice(alpha) for _ in range(lens[t % len(lens)]))
+        h = O.huffman_enc(s)
+        if corrupt is not None:
+            h = corrupt(t, bytearray(h))
+        pos = rng.randrange(64)
+        strs += short[:pos] + [bytes(h)] + short[pos:]
+    return pack(strs)
+
+
+@pytest.mark.parametrize("alpha", ["token", "all", "long"])
+def test_decode_cooperative_long_strings(codec, alpha):
+    """Strings above the cooperative threshold (128 Huffman bytes) are
+    decoded by the whole wave (segment walks, meeting points, counts, then
+    the write walk): lengths around the threshold and the segment sizes, up
+    to the stage's whole span, each in a tile of short strings; bit-exact
+    against the oracle."""
+    rng = random.Random(len(alpha) * 31)
+    lens = [150, 160, 161, 170, 200, 256, 300, 480, 700, 1000, 1461, 1900, 2400]
+    if alpha == "all":
+        lens = [80, 81, 100, 130, 200, 400, 700, 900]   # ~2.6x expansion
+    data, off = _long_tiles(rng, 3 * len(lens), lens, ALPHAS[alpha])
+    out, oo, st = check_decode(codec, data, off)
+    assert not st.any()
+    check_decode(codec, data, off, pad_front=7)
+
+
+def test_decode_cooperative_invalid(codec):
+    """Invalid long strings (an EOS code inside, a flipped bit, non-ones or
+    over-long padding, a cut string) take the one-lane decode again: status
+    and bytes as the reference decoder."""
+    rng = random.Random(4242)
+
+    def corrupt(i, h):
+        k = i % 6
+        if k == 0:                                   # EOS at a byte boundary
+            at = rng.randrange(len(h) // 4, len(h) // 2)
+            h[at:at] = b"\xff\xff\xff\xfc"
+        elif k == 1:
+            at = rng.randrange(len(h))
+            h[at] ^= 1 << rng.randrange(8)
+        elif k == 2:
+            h[-1] &= 0xfe                            # non-ones padding (often)
+        elif k == 3:
+            h += b"\xff"                             # padding of >= 8 bits
+        elif k == 4:
+            h = h[:-3]                               # cut
+        return h
+
+    data, off = _long_tiles(rng, 120, [200, 500, 1200], ALPHAS["token"],
+                            corrupt)
+    out, oo, st = check_decode(codec, data, off)
+    assert st.sum() > 20 and (st == 0).sum() > 1000
+
+
 def _launch_shape_check(c, n, seed):
     import qhuff
     data, off = qhuff.synth_batch(n, seed=seed)

@@ -4,9 +4,10 @@ each launch timed by its own dispatch timestamps (qhuff_timing_*, ABI 4;
 HIP events per launch for older libraries), so box-to-box and
 process-to-process variance cancel.  Prints per-library median and mean
 kernel times for encode and decode of the bench workload (1,048,576 token
-strings, 8-64 B).
+strings, 8-64 B), or with WORKLOAD=corpus / alphabet_c of bench.py's
+real-workload legs (qhuff/workload.py).
 
-usage: python tools/ab_inproc.py LIB_A LIB_B [rounds] [per_block]"""
+usage: [WORKLOAD=...] python tools/ab_inproc.py LIB_A LIB_B [rounds] [per_block]"""
 import ctypes as C
 import json
 import os
@@ -47,7 +48,16 @@ def main():
     per = int(sys.argv[4]) if len(sys.argv) > 4 else 10
     n = 1 << 20
     dev = torch.device("cuda", 0)
-    data, off = qhuff.synth_batch(n, seed=0x9E3779B97F4A7C15)
+    wl = os.environ.get("WORKLOAD", "synthetic")
+    if wl == "corpus":
+        from qhuff import workload
+        data, off = workload.corpus_batch(
+            n, os.path.join(ROOT, "tests", "golden", "data"))
+    elif wl == "alphabet_c":
+        from qhuff import workload
+        data, off = workload.alphabet_c(n)
+    else:
+        data, off = qhuff.synth_batch(n, seed=0x9E3779B97F4A7C15)
     raw = int(off[-1])
     d_in = torch.from_numpy(data).to(dev)
     d_off = torch.from_numpy(off.view(np.int32)).to(dev)
@@ -108,7 +118,7 @@ def main():
                 times[(k, op)] += [ev[i].elapsed_time(ev[i + 1]) * 1e3
                                    for i in range(per)]
     ok = (torch.equal(d_out[:raw], d_in) and bool((d_st == 0).all()))
-    res = {"ok": ok, "rounds": rounds, "per_block": per}
+    res = {"ok": ok, "workload": wl, "rounds": rounds, "per_block": per}
     for k, name in enumerate("ab"):
         for op in ("enc", "dec"):
             t = times[(k, op)]
