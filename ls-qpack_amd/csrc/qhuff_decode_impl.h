@@ -458,9 +458,10 @@ write_bytes(QH_LDS uint8_t *d, uint32_t v, uint32_t nb)
 // One lane walks one string: a tile's time is its longest string's.  On the
 // reference's own header corpora (tests/golden/data/*.qif) a tile's longest
 // string is ~13x its mean one (cookies, user agents, 1,461-byte values), so
-// the lanes idle.  A string of more than kCoopMin Huffman bytes is decoded
-// by the whole wave instead, its bits cut into segments of S bits (a
-// multiple of 32, >= kSegMin, at most 64 segments), one per lane:
+// the lanes idle.  The strings of more than kCoopMin Huffman bytes are
+// decoded by the whole wave instead, all of a tile's at once: their bits cut
+// into segments of S bits (a multiple of 32, >= kSegMin, at most 64
+// segments in all), one per lane:
 //   A  every lane walks its segment from the segment's first bit -- a guess:
 //      only lane 0 starts on a code boundary -- and marks the bit of each
 //      symbol start it passes in a bitmap (one bit per input bit);
@@ -654,36 +655,65 @@ bm_count(const QH_LDS uint32_t *bm, uint32_t r0, uint32_t r1)
     return c;
 }
 
-// Decode the string at bits [b0, b1) of the stage with the whole wave, into
-// the arena bytes at `slot` (every lane gets the result).  bm: a zeroed-on-
-// entry bitmap of (b1 - b0) / 32 + 2 words; sink: kCoopDummy bytes.
-// Returns the output length, or -1 when the one-lane decode must do it (an
-// invalid string, or any disagreement).
+// Decode the strings of the tile flagged in `coop` (lane j: its string at
+// bytes [rs, re) of the stage, its arena slot at arena + slot) with the whole
+// wave at once: string j gets max(1, bits_j / S) segments of S bits (lanes
+// in string order; S a multiple of 32, >= kSegMin, small enough that the
+// segments fit 64 lanes), its bitmap at word bmw of bms (zeroed here, bits_j
+// / 32 + 2 words) -- A, B, the counts and W as above, each lane on its own
+// string.  sink: kCoopDummy bytes.  Returns, in lane j, string j's output
+// length, or -1 when its own lane must decode it (an invalid string, or any
+// disagreement); 0 elsewhere.
 __device__ __forceinline__ int
-coop_decode(const QH_LDS uint32_t *src, uint32_t b0, uint32_t b1,
-            QH_LDS uint8_t *slot, QH_LDS uint32_t *bm, QH_LDS uint8_t *sink,
+coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
+            uint32_t re, uint32_t slot, QH_LDS uint8_t *arena,
+            QH_LDS uint32_t *bms, QH_LDS uint8_t *sink,
             const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted)
 {
     const uint32_t lane = lane_id();
-    const uint32_t nbits = b1 - b0;
-    uint32_t S = (((nbits + 63) >> 6) + 31) & ~31u;
+    const bool mine = (coop >> lane) & 1;
+    const uint32_t nb = mine ? 8 * (re - rs) : 0u;
+    const uint32_t ncoop = (uint32_t) __builtin_popcountll(coop);   // < 64
+    // sum_j max(1, nb_j / S) <= tot / S + ncoop <= 64
+    const uint32_t tot = read_lane(wave_incl_scan(nb), 63);
+    const uint32_t dv = 64 - ncoop;
+    uint32_t S = ((((tot + dv - 1) / dv) + 31) & ~31u);
     S = S > kSegMin ? S : kSegMin;
-    const uint32_t nseg = nbits / S > 0 ? nbits / S : 1u;   // <= 64
-    const bool act = lane < nseg;
-    const uint32_t s = act ? b0 + lane * S : b1;
-    const uint32_t stop = lane + 1 < nseg ? s + S : b1;
-    const uint32_t nw = nbits / 32 + 2;
-    for (uint32_t i = lane; i < nw; i += 64)
-        bm[i] = 0;
+    const uint32_t ns = mine ? (nb / S > 0 ? nb / S : 1u) : 0u;
+    const uint32_t g = wave_incl_scan(ns) - ns;           // first segment lane
+    const uint32_t wds = mine ? nb / 32 + 2 : 0u;
+    const uint32_t wincl = wave_incl_scan(wds);
+    const uint32_t nwords = read_lane(wincl, 63);
+    // this lane's string j and segment q
+    uint32_t j = lane, gj = 0, nsj = 0;
+    for (uint64_t m = coop; m; m &= m - 1)
+    {
+        const uint32_t c = (uint32_t) __builtin_ctzll(m);
+        const uint32_t gc = read_lane(g, c), nc = read_lane(ns, c);
+        const bool in = lane - gc < nc;
+        j = in ? c : j;
+        gj = in ? gc : gj;
+        nsj = in ? nc : nsj;
+    }
+    const bool act = nsj != 0;
+    const uint32_t q = lane - gj;
+    const uint32_t b0 = act ? 8 * (uint32_t) __shfl((int) rs, (int) j, 64) : 0u;
+    const uint32_t b1 = act ? 8 * (uint32_t) __shfl((int) re, (int) j, 64) : 0u;
+    QH_LDS uint8_t *sl = arena + (uint32_t) __shfl((int) slot, (int) j, 64);
+    QH_LDS uint32_t *bm = bms + (uint32_t) __shfl((int) (wincl - wds), (int) j, 64);
+    const uint32_t s = act ? b0 + q * S : 0u;
+    const uint32_t stop = !act ? 0u : q + 1 < nsj ? s + S : b1;
+    for (uint32_t i = lane; i < nwords; i += 64)
+        bms[i] = 0;
     wave_sync();
     // A: guessed walks, marking
     uint32_t E = s, C = 0, h = 0;
     seg_walk<kWalkMark>(src, E, stop, b1, s_win, s_sorted, bm, b0, nullptr,
                         nullptr, sink, C, h);
     wave_sync();
-    // B: walk on into the next segment until meeting its marks
-    const bool cl = act & (lane + 1 < nseg);
-    const uint32_t lim2 = !cl ? b1 : lane + 2 < nseg ? s + 2 * S : b1;
+    // B: walk on into the next segment of the string until meeting its marks
+    const bool cl = act & (q + 1 < nsj);
+    const uint32_t lim2 = !cl ? b1 : q + 2 < nsj ? s + 2 * S : b1;
     uint32_t cs = E, X = 0, K = 0, met = 0;
     bool redo = cl;
     uint32_t pm = 0, px = 0, rounds = 0;
@@ -695,36 +725,42 @@ coop_decode(const QH_LDS uint32_t *src, uint32_t b0, uint32_t b1,
         X = redo ? x : X;
         K = redo ? k : K;
         met = redo ? hm : met;
-        // lane j >= 1: its exact exit is its own (lane j - 1 met its walk)
-        // or lane j - 1's walk's
+        // segment q >= 1: its exact exit is its own (segment q - 1's walk met
+        // its marks) or segment q - 1's walk's end
         pm = wave_shr1(met);
         px = wave_shr1(X);
-        const uint32_t tE = (lane >= 1 && !pm) ? px : E;
+        const uint32_t tE = (q >= 1 && !pm) ? px : E;
         redo = cl & (tE != cs);
         cs = cl ? tE : cs;
-        if (++rounds > 64)                   // (cannot happen: a lane's exit
-            return -1;                       // is fixed after j rounds)
+        if (++rounds > 64)                   // (cannot happen: segment q's
+            return mine ? -1 : 0;            // exit is fixed after q rounds)
     }
-    // symbols of each segment
+    // symbols of each segment, offsets within the string
     const uint32_t kp = wave_shr1(K);
-    const uint32_t own = bm_count(bm, (act && lane >= 1 && pm) ? px - b0 : 0u,
-                                  (act && lane >= 1 && pm) ? stop - b0 : 0u);
-    const uint32_t T = !act ? 0u : lane == 0 ? C : kp + own;
+    const bool cnt_own = act && q >= 1 && pm;
+    const uint32_t own = bm_count(bm, cnt_own ? px - b0 : 0u,
+                                  cnt_own ? stop - b0 : 0u);
+    const uint32_t T = !act ? 0u : q == 0 ? C : kp + own;
     const uint32_t incl = wave_incl_scan(T);
-    const uint32_t N = read_lane(incl, 63);
-    if (N > (8 * (nbits >> 3)) / 5)          // more than the slot holds
-        return -1;
+    const uint32_t base = (uint32_t) __shfl((int) (incl - T), (int) gj, 64);
+    const uint32_t N = (uint32_t) __shfl((int) incl, (int) (gj + nsj - 1), 64)
+                     - base;
+    const bool big = N > (8 * ((b1 - b0) >> 3)) / 5;   // more than the slot
     // W: decode from the exact first symbol starts
-    const uint32_t ts = lane == 0 ? b0 : wave_shr1(cs);
-    uint32_t x = act ? ts : b1, m = 0, bad = 0;
-    seg_walk<kWalkEmit>(src, x, act ? stop : b1, b1, s_win, s_sorted, bm, b0,
-                        slot + (incl - T), slot + N, sink + lane, m, bad);
-    // each exit must be the next segment's start; the last one the end
+    const uint32_t ts = q == 0 ? b0 : wave_shr1(cs);
+    const bool wr = act & !big;
+    uint32_t x = wr ? ts : b1, m = 0, bad = 0;
+    seg_walk<kWalkEmit>(src, x, wr ? stop : b1, b1, s_win, s_sorted, bm, b0,
+                        sl + (incl - T - base), sl + N, sink + lane, m, bad);
+    // each exit must be the next segment's start
     const uint32_t nts = (uint32_t) __shfl_down((int) ts, 1, 64);
-    const bool chain = !act || (lane + 1 < nseg ? x == nts : true);
-    if (__builtin_amdgcn_ballot_w64(act & ((m != T) | (bad != 0) | !chain)))
-        return -1;
-    return (int) N;
+    const bool chain = q + 1 < nsj ? x == nts : true;
+    const uint64_t fb = __builtin_amdgcn_ballot_w64(
+        act & (big | (m != T) | (bad != 0) | !chain));
+    // lane j: its string's segments gj .. gj + nsj - 1 (its own g, ns)
+    const uint64_t segm = ns >= 64 ? ~0ull : ((1ull << ns) - 1) << g;
+    const uint32_t Nj = (uint32_t) __shfl((int) N, (int) g, 64);
+    return !mine ? 0 : (fb & segm) ? -1 : (int) Nj;
 }
 
 // copy n bytes src -> dst (LDS) with the whole wave: whole dwords at dst,
@@ -912,38 +948,31 @@ struct DecPolicyT
         // bitmap (hl / 4 + 2 words) and the sinks go above them
         const uint32_t slots_end = 2 * kDecTS
                                  + (uint32_t) ((8ull * (to.last() - A)) / 5) + 2;
-        const bool lng = !fixed && (lane < cnt) && hl > kCoopMin
-                      && slots_end + 4 * (hl / 4 + 2) + kCoopDummy
-                             <= (uint32_t) kArenaBytes;
+        // candidates in lane order while their bitmaps fit (at most 48)
+        const bool cand = !fixed && (lane < cnt) && hl > kCoopMin;
+        const uint32_t bmb = cand ? 4 * (hl / 4 + 2) : 0u;
+        const uint32_t bm0 = (slots_end + 3) & ~3u;
+        const bool lng = cand && bm0 + wave_incl_scan(bmb) + kCoopDummy
+                                     <= (uint32_t) kArenaBytes;
         coop = __builtin_amdgcn_ballot_w64(lng);
+        if (__builtin_popcountll(coop) > 48)
+            coop = 0;
+        const bool mine = (coop >> lane) & 1;
         int r = 0;
         if (lane < cnt)
         {
             ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
-            r = decode_string_lds(wv->in, 8 * rs, lng ? 8 * rs : 8 * re,
+            r = decode_string_lds(wv->in, 8 * rs, mine ? 8 * rs : 8 * re,
                                   sm->win, sm->sorted, em);
         }
         if (coop)
         {
-            QH_LDS uint8_t *sink = wv->arena + kArenaBytes - kCoopDummy;
-            uint64_t m = coop, fail = 0;
-            while (m)
-            {
-                const uint32_t j = (uint32_t) __builtin_ctzll(m);
-                m &= m - 1;
-                const uint32_t b0 = 8 * read_lane(rs, j);
-                const uint32_t b1 = 8 * read_lane(re, j);
-                const uint32_t nw = (b1 - b0) / 32 + 2;
-                QH_LDS uint32_t *bm =
-                    (QH_LDS uint32_t *) (sink - 4 * nw);
-                const int rc = coop_decode(wv->in, b0, b1,
-                                           wv->arena + read_lane(slot0, j), bm,
-                                           sink, sm->win, sm->sorted);
-                if (rc < 0)
-                    fail |= 1ull << j;
-                else
-                    r = lane == j ? rc : r;
-            }
+            const int rc = coop_decode(
+                wv->in, coop, rs, re, slot0, wv->arena,
+                (QH_LDS uint32_t *) (wv->arena + bm0),
+                wv->arena + kArenaBytes - kCoopDummy, sm->win, sm->sorted);
+            r = mine ? rc : r;
+            const uint64_t fail = __builtin_amdgcn_ballot_w64(mine & (rc < 0));
             if (fail)
             {
                 // (rare) an invalid string: its own lane decodes it again

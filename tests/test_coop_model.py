@@ -50,18 +50,28 @@ def _walker(h):
     return at
 
 
-def coop_model(h):
-    """(output bytes, rounds) of coop_decode for the Huffman string h, or
-    None where the kernel falls back to the one-lane decode."""
+def seg_bits(hls):
+    """S for a tile whose cooperative strings have these Huffman lengths:
+    the kernel's sum_j max(1, bits_j / S) <= 64 choice"""
+    tot = 8 * sum(hls)
+    dv = 64 - len(hls)
+    return max(SEG_MIN, (((tot + dv - 1) // dv) + 31) & ~31)
+
+
+def coop_model(h, S=None):
+    """(output bytes, rounds) of coop_decode for the Huffman string h (alone
+    in its tile unless S is given), or None where the kernel falls back to
+    the one-lane decode."""
     at = _walker(h)
     b1 = nbits = 8 * len(h)
+    if S is None:
+        S = seg_bits([len(h)])
     hv = int.from_bytes(h, "big")
 
     def pad_bad(pos):
         """the D3 rule on the bits [pos, b1) after the last symbol"""
         r = b1 - pos
         return r >= 8 or (hv & ((1 << r) - 1)) != (1 << r) - 1
-    S = max(SEG_MIN, ((((nbits + 63) >> 6) + 31) & ~31))
     nseg = max(1, nbits // S)
     assert nseg <= 64
     s = [k * S for k in range(nseg)]
@@ -151,6 +161,22 @@ def test_coop_model_corpus():
         assert r is not None and r[0] == s
         rounds.append(r[1])
     assert max(rounds) < 16
+
+
+def test_coop_model_tiles():
+    """Several cooperative strings of one tile share the lanes: S from all
+    of them, every string decoded right, never more than 64 segments."""
+    rng = random.Random(3)
+    long = sorted({s for s in corpus_strings() if len(O.huffman_enc(s)) > 128})
+    for _ in range(40):
+        k = rng.randint(1, 6)
+        strs = rng.sample(long, k)
+        hs = [O.huffman_enc(x) for x in strs]
+        S = seg_bits([len(h) for h in hs])
+        assert sum(max(1, 8 * len(h) // S) for h in hs) <= 64
+        for x, h in zip(strs, hs):
+            r = coop_model(h, S)
+            assert r is not None and r[0] == x
 
 
 @pytest.mark.parametrize("alpha", [b"abcdefghijklmnopqrstuvwxyz0123456789-_./",
