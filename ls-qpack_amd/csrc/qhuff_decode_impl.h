@@ -492,9 +492,20 @@ constexpr uint32_t kCoopMin = QH_COOP_MIN;      // Huffman bytes
 #endif
 constexpr uint32_t kSegMin = QH_SEG_MIN;        // bits per segment
 static_assert(kSegMin % 32 == 0 && kSegMin >= 64, "segment bits");
-constexpr uint32_t kCoopDummy = 64;             // per-lane sink bytes
+constexpr uint32_t kCoopDummy = 128;            // sink bytes, 2 per lane
 
 enum WalkMode { kWalkMark, kWalkCheck, kWalkEmit };
+
+// A cross-lane result (DPP, ds_bpermute), computed by every lane here: left
+// to itself the compiler may move the operation into the branch of a select
+// that uses it, where the lanes it reads from are off (and read as 0).
+template <class T>
+__device__ __forceinline__ T
+all_lanes(T v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 // Walk the symbols of the staged stream src that start at [pos, lim) of the
 // string ending at bitend (lim <= bitend; a walk that reaches the string's
@@ -675,14 +686,14 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
     const uint32_t nb = mine ? 8 * (re - rs) : 0u;
     const uint32_t ncoop = (uint32_t) __builtin_popcountll(coop);   // < 64
     // sum_j max(1, nb_j / S) <= tot / S + ncoop <= 64
-    const uint32_t tot = read_lane(wave_incl_scan(nb), 63);
+    const uint32_t tot = read_lane(all_lanes(wave_incl_scan(nb)), 63);
     const uint32_t dv = 64 - ncoop;
     uint32_t S = ((((tot + dv - 1) / dv) + 31) & ~31u);
     S = S > kSegMin ? S : kSegMin;
     const uint32_t ns = mine ? (nb / S > 0 ? nb / S : 1u) : 0u;
-    const uint32_t g = wave_incl_scan(ns) - ns;           // first segment lane
+    const uint32_t g = all_lanes(wave_incl_scan(ns)) - ns;   // first segment
     const uint32_t wds = mine ? nb / 32 + 2 : 0u;
-    const uint32_t wincl = wave_incl_scan(wds);
+    const uint32_t wincl = all_lanes(wave_incl_scan(wds));
     const uint32_t nwords = read_lane(wincl, 63);
     // this lane's string j and segment q
     uint32_t j = lane, gj = 0, nsj = 0;
@@ -697,10 +708,15 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
     }
     const bool act = nsj != 0;
     const uint32_t q = lane - gj;
-    const uint32_t b0 = act ? 8 * (uint32_t) __shfl((int) rs, (int) j, 64) : 0u;
-    const uint32_t b1 = act ? 8 * (uint32_t) __shfl((int) re, (int) j, 64) : 0u;
-    QH_LDS uint8_t *sl = arena + (uint32_t) __shfl((int) slot, (int) j, 64);
-    QH_LDS uint32_t *bm = bms + (uint32_t) __shfl((int) (wincl - wds), (int) j, 64);
+    const uint32_t rsj = all_lanes((uint32_t) __shfl((int) rs, (int) j, 64));
+    const uint32_t rej = all_lanes((uint32_t) __shfl((int) re, (int) j, 64));
+    const uint32_t slj = all_lanes((uint32_t) __shfl((int) slot, (int) j, 64));
+    const uint32_t bmj = all_lanes(
+        (uint32_t) __shfl((int) (wincl - wds), (int) j, 64));
+    const uint32_t b0 = act ? 8 * rsj : 0u;
+    const uint32_t b1 = act ? 8 * rej : 0u;
+    QH_LDS uint8_t *sl = arena + slj;
+    QH_LDS uint32_t *bm = bms + bmj;
     const uint32_t s = act ? b0 + q * S : 0u;
     const uint32_t stop = !act ? 0u : q + 1 < nsj ? s + S : b1;
     for (uint32_t i = lane; i < nwords; i += 64)
@@ -727,8 +743,8 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
         met = redo ? hm : met;
         // segment q >= 1: its exact exit is its own (segment q - 1's walk met
         // its marks) or segment q - 1's walk's end
-        pm = wave_shr1(met);
-        px = wave_shr1(X);
+        pm = all_lanes(wave_shr1(met));
+        px = all_lanes(wave_shr1(X));
         const uint32_t tE = (q >= 1 && !pm) ? px : E;
         redo = cl & (tE != cs);
         cs = cl ? tE : cs;
@@ -736,30 +752,58 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
             return mine ? -1 : 0;            // exit is fixed after q rounds)
     }
     // symbols of each segment, offsets within the string
-    const uint32_t kp = wave_shr1(K);
+    const uint32_t kp = all_lanes(wave_shr1(K));
     const bool cnt_own = act && q >= 1 && pm;
     const uint32_t own = bm_count(bm, cnt_own ? px - b0 : 0u,
                                   cnt_own ? stop - b0 : 0u);
     const uint32_t T = !act ? 0u : q == 0 ? C : kp + own;
-    const uint32_t incl = wave_incl_scan(T);
-    const uint32_t base = (uint32_t) __shfl((int) (incl - T), (int) gj, 64);
-    const uint32_t N = (uint32_t) __shfl((int) incl, (int) (gj + nsj - 1), 64)
+    const uint32_t incl = all_lanes(wave_incl_scan(T));
+    const uint32_t base = all_lanes((uint32_t) __shfl((int) (incl - T), (int) gj,
+                                                      64));
+    const uint32_t N = all_lanes((uint32_t) __shfl((int) incl,
+                                                   (int) (gj + nsj - 1), 64))
                      - base;
     const bool big = N > (8 * ((b1 - b0) >> 3)) / 5;   // more than the slot
     // W: decode from the exact first symbol starts
-    const uint32_t ts = q == 0 ? b0 : wave_shr1(cs);
+    const uint32_t pcs = all_lanes(wave_shr1(cs));
+    const uint32_t ts = q == 0 ? b0 : pcs;
     const bool wr = act & !big;
     uint32_t x = wr ? ts : b1, m = 0, bad = 0;
     seg_walk<kWalkEmit>(src, x, wr ? stop : b1, b1, s_win, s_sorted, bm, b0,
-                        sl + (incl - T - base), sl + N, sink + lane, m, bad);
+                        sl + (incl - T - base), sl + N, sink + 2 * lane, m,
+                        bad);
     // each exit must be the next segment's start
-    const uint32_t nts = (uint32_t) __shfl_down((int) ts, 1, 64);
+    const uint32_t nts = all_lanes((uint32_t) __shfl_down((int) ts, 1, 64));
     const bool chain = q + 1 < nsj ? x == nts : true;
     const uint64_t fb = __builtin_amdgcn_ballot_w64(
         act & (big | (m != T) | (bad != 0) | !chain));
     // lane j: its string's segments gj .. gj + nsj - 1 (its own g, ns)
     const uint64_t segm = ns >= 64 ? ~0ull : ((1ull << ns) - 1) << g;
-    const uint32_t Nj = (uint32_t) __shfl((int) N, (int) g, 64);
+#ifdef QH_COOP_DEBUG
+    // (diagnostic builds) a failing string's first failing segment, as 8
+    // u32 at its slot: reason bits, q, m, T, exit, next start, S, segments
+    for (uint64_t mm = coop; mm; mm &= mm - 1)
+    {
+        const uint32_t c = (uint32_t) __builtin_ctzll(mm);
+        const uint32_t gc = read_lane(g, c), nc = read_lane(ns, c);
+        const uint64_t sm_ = nc >= 64 ? ~0ull : ((1ull << nc) - 1) << gc;
+        if (fb & sm_)
+        {
+            const uint32_t f0 = (uint32_t) __builtin_ctzll(fb & sm_);
+            const uint32_t why = (read_lane(big ? 1u : 0u, f0))
+                               | (read_lane(m != T ? 2u : 0u, f0))
+                               | (read_lane(bad ? 4u : 0u, f0))
+                               | (read_lane(chain ? 0u : 8u, f0));
+            const uint32_t rec[8] = {why, read_lane(q, f0), read_lane(m, f0),
+                                     read_lane(T, f0), read_lane(x, f0),
+                                     read_lane(nts, f0), S, nc};
+            QH_LDS uint8_t *d = arena + read_lane(slot, c);
+            if (lane < 32)
+                d[lane] = (uint8_t) (rec[lane >> 2] >> (8 * (lane & 3)));
+        }
+    }
+#endif
+    const uint32_t Nj = all_lanes((uint32_t) __shfl((int) N, (int) g, 64));
     return !mine ? 0 : (fb & segm) ? -1 : (int) Nj;
 }
 
@@ -842,6 +886,9 @@ compact_wave(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
     write_bytes(dstb + it, vt, nt);
 }
 
+
+
+#if !QH_BIG_TILES
 // A tile whose input or output does not fit the stage, coded eagerly:
 // input staged -> the arena already holds the bytes (sz / st given);
 // otherwise count from global memory, then decode again to global.  The
@@ -852,7 +899,7 @@ compact_wave(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
 // decoded before its error (DecPolicyT).
 template <bool Keep, class SM, class BaseOf>
 __device__ __noinline__ uint64_t
-dec_slow_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
+dec_slow_tile_r3(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
               uint32_t slot0, uint32_t cnt, TileOffs to, Span sp, uint32_t sz,
               uint32_t st, uint8_t *out, uint32_t *t_off, uint8_t *t_status,
               BaseOf base_of)
@@ -897,6 +944,14 @@ dec_slow_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
     return base + total;
 }
 
+#endif
+
+template <bool Keep, class SM, class BaseOf>
+__device__ __forceinline__ uint64_t
+dec_big_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv, uint32_t cnt,
+             TileOffs to, Span sp, uint32_t sz, uint32_t st, uint32_t slot0,
+             uint8_t *out, uint32_t *t_off, uint8_t *t_status, BaseOf base_of);
+
 // the decode side of the wave pipeline (qhuff_pipeline.h, qhuff_service.hip);
 // SM: the workgroup's LDS (win, sorted).  Keep (the kernel the per-string
 // entry points use to replay where the reference stops on an invalid
@@ -935,31 +990,43 @@ struct DecPolicyT
                                           const Span &sp, uint32_t *sz,
                                           uint32_t *st)
     {
+        codec_range(to, 0, cnt, sp, sz, st);
+    }
+    // the strings of lanes [lo, hi) (sp: their span)
+    __device__ __forceinline__ void codec_range(const Offs &to, uint32_t lo,
+                                                uint32_t cnt, const Span &sp,
+                                                uint32_t *sz, uint32_t *st)
+    {
         const uint32_t lane = lane_id();
-        const uint32_t A = to.first();
+        const bool valid = (lane >= lo) & (lane < cnt);
+        const uint32_t A = read_lane(to.o0, lo);
         const uint32_t hl = to.o1 - to.o0;
         const bool fixed = !__builtin_amdgcn_ballot_w64(
-            (lane < cnt) & (hl > kFixMaxLen));
+            valid & (hl > kFixMaxLen));
         slot0 = fixed ? kFixStride * lane
                       : 2 * lane + (uint32_t) ((8ull * (to.o0 - A)) / 5);
         const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
         const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
         // the slots end below kVarArenaBytes - slack + 1 for this span; the
         // bitmap (hl / 4 + 2 words) and the sinks go above them
-        const uint32_t slots_end = 2 * kDecTS
-                                 + (uint32_t) ((8ull * (to.last() - A)) / 5) + 2;
+        const uint32_t slots_end =
+            2 * kDecTS + (uint32_t) ((8ull * (read_lane(to.o1, cnt - 1) - A)) / 5)
+            + 2;
         // candidates in lane order while their bitmaps fit (at most 48)
-        const bool cand = !fixed && (lane < cnt) && hl > kCoopMin;
+        const bool cand = !fixed && valid && hl > kCoopMin;
         const uint32_t bmb = cand ? 4 * (hl / 4 + 2) : 0u;
         const uint32_t bm0 = (slots_end + 3) & ~3u;
-        const bool lng = cand && bm0 + wave_incl_scan(bmb) + kCoopDummy
-                                     <= (uint32_t) kArenaBytes;
+        const uint32_t bmi = all_lanes(wave_incl_scan(bmb));
+        const bool lng = cand & (bm0 + bmi + kCoopDummy <= (uint32_t) kArenaBytes);
         coop = __builtin_amdgcn_ballot_w64(lng);
         if (__builtin_popcountll(coop) > 48)
             coop = 0;
         const bool mine = (coop >> lane) & 1;
         int r = 0;
-        if (lane < cnt)
+#ifdef QH_COOP_DEBUG
+        bool dbg_fb = false;
+#endif
+        if (valid)
         {
             ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
             r = decode_string_lds(wv->in, 8 * rs, mine ? 8 * rs : 8 * re,
@@ -973,12 +1040,27 @@ struct DecPolicyT
                 wv->arena + kArenaBytes - kCoopDummy, sm->win, sm->sorted);
             r = mine ? rc : r;
             const uint64_t fail = __builtin_amdgcn_ballot_w64(mine & (rc < 0));
+#ifdef QH_COOP_DEBUG
             if (fail)
             {
+                const bool f = (fail >> lane) & 1;
+                r = f ? 32 : r;
+                dbg_fb = f;
+                coop &= ~fail;
+            }
+            if (false)
+#else
+            if (fail)
+#endif
+            {
                 // (rare) an invalid string: its own lane decodes it again
+                // (the other lanes' two stores go to their sink bytes)
                 coop &= ~fail;
                 const bool f = (fail >> lane) & 1;
-                ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
+                QH_LDS uint8_t *d0 = f ? wv->arena + slot0
+                                       : wv->arena + kArenaBytes - kCoopDummy
+                                             + 2 * lane;
+                ArenaEmit em{d0, d0, 0};
                 const int r2 = decode_string_lds(wv->in, 8 * rs,
                                                  f ? 8 * re : 8 * rs, sm->win,
                                                  sm->sorted, em);
@@ -987,6 +1069,9 @@ struct DecPolicyT
         }
         *sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
         *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+#ifdef QH_COOP_DEBUG
+        *st = dbg_fb ? 7u : *st;
+#endif
     }
     // arena -> the (dead) input stage, compacted (the cooperative strings
     // by the whole wave, after the rest)
@@ -1013,16 +1098,23 @@ struct DecPolicyT
     }
 
     // a tile of the batch kernel: base from the look-back
+    template <class BaseOf>
     __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
                                               Offs to, Span sp, uint32_t sz,
                                               uint32_t st, uint8_t *out,
                                               uint32_t *out_off, uint8_t *status,
-                                              uint64_t n)
+                                              uint64_t n, BaseOf base_of)
     {
         const uint64_t s0 = (uint64_t) t * kTS;
-        const uint64_t end = dec_slow_tile<Keep>(in, sm, wv, slot0, cnt, to, sp, sz,
-                                           st, out, out_off + s0, status + s0,
-                                           LookBackBase{c, t});
+#if QH_BIG_TILES
+        const uint64_t end = dec_big_tile<Keep>(in, sm, wv, cnt, to, sp, sz, st,
+                                                slot0, out, out_off + s0,
+                                                status + s0, base_of);
+#else
+        const uint64_t end = dec_slow_tile_r3<Keep>(in, sm, wv, slot0, cnt, to,
+                                                    sp, sz, st, out, out_off + s0,
+                                                    status + s0, base_of);
+#endif
         last_tile_end(c, t, end, out_off, n);
     }
     // a tile at a known base
@@ -1032,9 +1124,191 @@ struct DecPolicyT
                                                      uint32_t *t_off,
                                                      uint8_t *t_status)
     {
-        return dec_slow_tile<Keep>(in, sm, wv, slot0, cnt, to, sp, sz, st, out, t_off,
-                             t_status, FixedBase{base});
+#if QH_BIG_TILES
+        return dec_big_tile<Keep>(in, sm, wv, cnt, to, sp, sz, st, slot0, out,
+                                  t_off, t_status, FixedBase{base});
+#else
+        return dec_slow_tile_r3<Keep>(in, sm, wv, slot0, cnt, to, sp, sz, st,
+                                      out, t_off, t_status, FixedBase{base});
+#endif
     }
 };
+
+// A tile whose input or output does not fit the stages, coded eagerly
+// in units -- runs of its strings whose input (and output) fit the
+// stages: each staged and decoded like a fast tile.  Sizes first (unit
+// by unit; given when the whole input was staged), then the base
+// (base_of: the batch kernel's look-back, or the service's running
+// offset), then every unit again, compacted and stored.  A string whose
+// input alone exceeds the stage is walked in global memory by its lane;
+// one whose output alone exceeds it is decoded in the arena and copied
+// out by the wave.  Offsets and statuses go to t_off / t_status (the
+// tile's first string).  Returns base + total.  Out of line (cold).
+// (A free function with its own policy object: a member called out of
+// line would take the address of the pipeline's policy, and the kernel's
+// hot loop would then keep its fields in scratch memory.)
+template <bool Keep, class SM, class BaseOf>
+__device__ __forceinline__ uint64_t
+dec_big_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
+             uint32_t cnt, TileOffs to, Span sp, uint32_t sz, uint32_t st,
+             uint32_t slot0, uint8_t *out, uint32_t *t_off, uint8_t *t_status,
+             BaseOf base_of)
+{
+    using P = DecPolicyT<SM, Keep>;
+    constexpr int kInCap = P::kInCap, kOutCap = P::kOutCap, kNch = P::kNch;
+    P pol{in, sm, wv, 0};
+    const uint32_t lane = lane_id();
+    const bool valid = lane < cnt;
+    auto stage = [&](uint32_t i0, uint32_t i1) -> Span {
+        const Span su = tile_span(in, read_lane(to.o0, i0),
+                                  read_lane(to.o1, i1 - 1), kInCap);
+        stage_chunks<true>(su, (QH_LDS u32x4 *) wv->in);
+        return su;
+    };
+    // a string beyond the stage, in global memory
+    auto glb = [&](uint32_t i, uint8_t *dst, uint32_t *n) -> int {
+        const uintptr_t pa = (uintptr_t) (in + read_lane(to.o0, i))
+                           & ~(uintptr_t) 15;
+        const DecGlb src{(const QH_GLB uint32_t *) pa};
+        const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - pa);
+        const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - pa);
+        int r = 0;
+        if (lane == i)
+        {
+            if (dst)
+            {
+                GlobalEmit em{dst, 0};
+                r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted,
+                                  em);
+            }
+            else
+            {
+                CountEmit em{0};
+                r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted,
+                                  em);
+            }
+        }
+        (void) n;
+        return r;
+    };
+#ifdef QH_SKIP_SLOW
+    // (timing experiments only: big tiles coded as empty -- wrong output)
+    {
+        const uint64_t b0 = base_of(0);
+        if (valid)
+            ((QH_GLB uint32_t *) t_off)[lane] = (uint32_t) b0;
+        return b0;
+    }
+#endif
+    // sizes
+    if (!sp.staged)
+    {
+        sz = 0;
+        st = 0;
+        for (uint32_t i0 = 0; i0 < cnt;)
+        {
+            const uint32_t k = unit_len(in, to, i0, cnt, kInCap, false, 0,
+                                        0, 0);
+            int r = 0;
+            if (k == 0)
+            {
+                r = glb(i0, nullptr, nullptr);
+                if (lane != i0)
+                    r = 0;
+            }
+            else
+            {
+                const Span su = stage(i0, i0 + k);
+                uint32_t s1, t1;
+                pol.codec_range(to, i0, i0 + k, su, &s1, &t1);
+                r = t1 == QHUFF_DEC_OK ? (int) s1
+                                       : -1 - (Keep ? (int) s1 : 0);
+                wave_sync();
+            }
+            const uint32_t kk = k ? k : 1u;
+            const bool in_u = (lane >= i0) & (lane < i0 + kk);
+            if (in_u)
+            {
+                sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
+                st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+            }
+            i0 += kk;
+        }
+    }
+    sz = valid ? sz : 0u;
+    const uint32_t incl = wave_incl_scan(sz);
+    const uint32_t excl = incl - sz;
+    const uint32_t total = read_lane(incl, 63);
+    const uint64_t base = base_of(total);
+    if (sp.staged)
+    {
+        // the tile was decoded whole into the arena (slot0): only its
+        // output overflows the stage -- copied out from there, the long
+        // strings by the whole wave, the others by their lanes
+        const bool lng = valid & (sz > 64);
+        if (valid && !lng && (Keep || st == QHUFF_DEC_OK))
+        {
+            const QH_LDS uint8_t *sa = wv->arena + slot0;
+            uint8_t *d = out + base + excl;
+            for (uint32_t i = 0; i < sz; ++i)
+                ((QH_GLB uint8_t *) d)[i] = sa[i];
+        }
+        for (uint64_t m = __builtin_amdgcn_ballot_w64(lng); m; m &= m - 1)
+        {
+            const uint32_t j = (uint32_t) __builtin_ctzll(m);
+            copy_out(wv->arena + read_lane(slot0, j),
+                     out + base + read_lane(excl, j), read_lane(sz, j));
+        }
+    }
+    // outputs, unit by unit
+    for (uint32_t i0 = 0; i0 < (sp.staged ? 0u : cnt);)
+    {
+        const uint32_t k = unit_len(in, to, i0, cnt, kInCap, true, excl, sz,
+                                    kOutCap);
+        const uint32_t e0 = read_lane(excl, i0);
+        if (k == 0)
+        {
+            // one string: input beyond the stage -> global walk; output
+            // beyond it -> the arena, copied out by the wave
+            const uint32_t si = read_lane(sz, i0);
+            const uint32_t sti = read_lane(st, i0);
+            if (unit_len(in, to, i0, cnt, kInCap, false, 0, 0, 0) == 0)
+            {
+                if (si && (Keep || sti == QHUFF_DEC_OK))
+                    glb(i0, out + base + e0, nullptr);
+            }
+            else if (si && (Keep || sti == QHUFF_DEC_OK))
+            {
+                const Span su = stage(i0, i0 + 1);
+                uint32_t s1, t1;
+                pol.codec_range(to, i0, i0 + 1, su, &s1, &t1);
+                wave_sync();
+                copy_out(wv->arena + read_lane(pol.slot0, i0), out + base + e0,
+                         si);
+            }
+            wave_sync();
+            i0 += 1;
+            continue;
+        }
+        const uint32_t i1 = i0 + k;
+        const Span su = stage(i0, i1);
+        uint32_t s1, t1;
+        pol.codec_range(to, i0, i1, su, &s1, &t1);
+        const bool in_u = (lane >= i0) & (lane < i1);
+        const uint32_t ul = read_lane(incl, i1 - 1) - e0;
+        wave_sync();
+        pol.emit(in_u ? excl - e0 : 0u, in_u ? s1 : 0u, ul);
+        wave_sync();
+        copy_out((const QH_LDS uint8_t *) wv->in, out + base + e0, ul);
+        wave_sync();
+        i0 = i1;
+    }
+    if (valid)
+    {
+        ((QH_GLB uint32_t *) t_off)[lane] = (uint32_t) (base + excl);
+        ((QH_GLB uint8_t *) t_status)[lane] = (uint8_t) st;
+    }
+    return base + total;
+}
 
 }  // namespace qhuff

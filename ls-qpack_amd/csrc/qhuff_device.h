@@ -668,6 +668,12 @@ struct TileOut
 {
     u32x4 o[NCH];
 
+    __device__ __forceinline__ void clear()
+    {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j)
+            o[j] = (u32x4){0, 0, 0, 0};
+    }
     __device__ __forceinline__ void gather(const QH_LDS uint32_t *stage)
     {
         const uint32_t lane = lane_id();

@@ -39,6 +39,14 @@
 
 #include "qhuff_kernels.h"
 
+// Big tiles (input or output past the stages) coded in staged units,
+// inline, their aggregate published before the pending tiles are flushed
+// (qhuff_*_impl.h *_big_tile); 0: the round-3 path, an out-of-line per-lane
+// walk over global memory after the pending tiles are flushed.
+#ifndef QH_BIG_TILES
+#define QH_BIG_TILES 1
+#endif
+
 namespace qhuff {
 
 constexpr int kChunks = 3;                  // 16-byte input chunks per lane
@@ -98,6 +106,71 @@ last_tile_end(const Coord &c, uint32_t t, uint64_t end, uint32_t *out_off,
         if (end > 0xffffffffull)                 // offsets are 32-bit
             raise_error(c, kErrRange);
     }
+}
+
+// (big tiles, qhuff_*_impl.h) the tile's lanes [i0, i0 + k) whose 16-byte-aligned input span fits the
+// stage (and, with outputs, whose output leaves 64 bytes of it free): k
+// (offsets ascend, so they are a prefix of the lanes from i0)
+__device__ __forceinline__ uint32_t
+unit_len(const uint8_t *in, const TileOffs &to, uint32_t i0, uint32_t cnt,
+         uint32_t cap, bool outs, uint32_t excl, uint32_t sz, uint32_t ocap)
+{
+    const uint32_t lane = lane_id();
+    const uintptr_t pa = (uintptr_t) (in + read_lane(to.o0, i0)) & ~(uintptr_t) 15;
+    const uintptr_t pe = ((uintptr_t) (in + to.o1) + 15) & ~(uintptr_t) 15;
+    const uint32_t e0 = read_lane(excl, i0);
+    const bool fit = (lane >= i0) & (lane < cnt) & (pe - pa <= (uintptr_t) cap)
+                   & (!outs | (excl + sz - e0 + 64 <= ocap));
+    return (uint32_t) __builtin_popcountll(__builtin_amdgcn_ballot_w64(fit));
+}
+
+// n bytes of LDS at src -> global dst (any alignment), the whole wave:
+// 16-byte stores (unaligned-access mode, as TileOut::store), the last < 16
+// bytes one per lane
+__device__ __forceinline__ void
+copy_out(const QH_LDS uint8_t *src, uint8_t *dst, uint32_t n)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t sa = (uint32_t) (uintptr_t) src, r = sa & 3;
+    const QH_LDS uint32_t *sw = (const QH_LDS uint32_t *) (src - r);
+    const uint32_t n16 = n >> 4;
+    for (uint32_t i = lane; i < n16; i += 64)
+    {
+        const QH_LDS uint32_t *w = sw + 4 * i;
+        const uint32_t a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
+        ((QH_GLB U4 *) (dst + 16 * i))->v =
+            (u32x4){align_bytes(b, a, r), align_bytes(c, b, r),
+                    align_bytes(d, c, r), align_bytes(e, d, r)};
+    }
+    const uint32_t t = 16 * n16 + lane;
+    if (lane < 16 && t < n)
+        ((QH_GLB uint8_t *) dst)[t] = src[t];
+}
+
+// a span's (<= 3 KB) 16-byte chunks global -> LDS (big tiles,
+// qhuff_*_impl.h): the lane's three loads issued together, then stored
+template <bool SWAP>
+__device__ __forceinline__ void
+stage_chunks(const Span &sp, QH_LDS u32x4 *dst)
+{
+    const uint32_t l = lane_id();
+    const uint32_t last = sp.n16 ? sp.n16 - 1 : 0;
+    const QH_GLB u32x4 *src = (const QH_GLB u32x4 *) sp.pa;
+    u32x4 v[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        v[k] = src[min(l + 64u * k, last)];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (l + 64u * k < sp.n16)
+        {
+            u32x4 x = v[k];
+            if (SWAP)
+                x = (u32x4){bswap32(x.x), bswap32(x.y), bswap32(x.z),
+                            bswap32(x.w)};
+            dst[l + 64u * k] = x;
+        }
+    wave_sync();
 }
 
 // resolve a pending tile's base and store it from `o` (every lane)
@@ -351,6 +424,8 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     {
         prof_stamp(c, it, 0);
         prof_realtime(c, it, 11);            // 100 MHz: the shader clock
+        if (it < 7)
+            prof_value(c, it + 8, 5, t);     // (profiling) the tile id
         // top: t's input, offsets and ticket were issued a codec ago and have
         // landed at the last iteration's poll wait; what is still in flight
         // here is that iteration's flush (stores, flag store, super publish),
@@ -461,6 +536,43 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
 
         if (fast)
             outs[D - 1].gather(pol.out_stage());
+#if QH_BIG_TILES
+        else
+        {
+            // A big tile (P::slow_tile: sizes, then the base, then the
+            // output).  Its aggregate is published as soon as its sizes are
+            // known, and only then are the pending tiles flushed: a flush
+            // waits on earlier tiles, other big tiles among them, so flushing
+            // first would chain the big tiles of the batch one after another.
+            auto base_of = [&](uint32_t total) -> uint64_t {
+                prof_stamp(c, kProfIters - 1, 1);
+                LookBack lb;
+                lb.start(c, t, total);
+#pragma unroll
+                for (int i = 0; i < D; ++i)
+                    if (pend[i].valid)
+                    {
+                        LookBack l = pend[i].lb();
+                        l.poll(c);
+                        flush_at(i, l, ~0u);
+                    }
+                // the flushed outputs are dead: constants in their registers
+                // (rematerialised, not kept) leave them to the output pass
+#pragma unroll
+                for (int i = 0; i < D; ++i)
+                    outs[i].clear();
+                lb.super_agg(c);
+                lb.poll(c);
+                const uint64_t b = lb.finish(c);
+                prof_stamp(c, kProfIters - 1, 2);
+                return b;
+            };
+            prof_stamp(c, kProfIters - 1, 0);    // (profiling) big tile
+            pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
+                          status, n, base_of);
+            prof_stamp(c, kProfIters - 1, 3);
+        }
+#else
         else
         {
             // (a slow tile only needs its predecessors' aggregates; the
@@ -475,8 +587,9 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
                     flush_at(i, l, ~0u);
                 }
             pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
-                          status, n);
+                          status, n, LookBackBase{c, t});
         }
+#endif
         wave_sync();
         prof_stamp(c, it, 6);
 

@@ -164,7 +164,13 @@ def slow_report(p, live):
 
 def main():
     n = int(os.environ.get("N", 1 << 20))
-    data, off = qhuff.synth_batch(n)
+    wl = os.environ.get("WORKLOAD", "synthetic")
+    if wl == "corpus":
+        from qhuff import workload
+        data, off = workload.corpus_batch(
+            n, os.path.join(ROOT, "tests", "golden", "data"))
+    else:
+        data, off = qhuff.synth_batch(n)
     dev = torch.device("cuda", 0)
     d = torch.from_numpy(data).to(dev)
     o = torch.from_numpy(off.view(np.int32)).to(dev)
