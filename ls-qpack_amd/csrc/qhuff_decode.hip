@@ -71,6 +71,9 @@ qhuff_decode_kernel(DecArgs a)
     prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
     DecPolicyT<DecSmem, Keep> pol{a.in, sm,
                                   &sm->w[__builtin_amdgcn_readfirstlane(tid >> 6)], 0};
+#ifdef QHUFF_PROFILE
+    pol.pc = &a.c;
+#endif
     uint32_t t0, k1, k2;
     wave_tickets(a.c, tk, &sm->tk, &t0, &k1, &k2);
     auto tables = [&]() {

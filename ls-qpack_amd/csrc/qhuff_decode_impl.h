@@ -496,16 +496,6 @@ constexpr uint32_t kCoopDummy = 128;            // sink bytes, 2 per lane
 
 enum WalkMode { kWalkMark, kWalkCheck, kWalkEmit };
 
-// A cross-lane result (DPP, ds_bpermute), computed by every lane here: left
-// to itself the compiler may move the operation into the branch of a select
-// that uses it, where the lanes it reads from are off (and read as 0).
-template <class T>
-__device__ __forceinline__ T
-all_lanes(T v)
-{
-    asm volatile("" : "+v"(v));
-    return v;
-}
 
 // Walk the symbols of the staged stream src that start at [pos, lim) of the
 // string ending at bitend (lim <= bitend; a walk that reaches the string's
@@ -679,8 +669,20 @@ __device__ __forceinline__ int
 coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
             uint32_t re, uint32_t slot, QH_LDS uint8_t *arena,
             QH_LDS uint32_t *bms, QH_LDS uint8_t *sink,
-            const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted)
+            const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
+            const Coord *pc = nullptr)
 {
+    // (profiling) the wave's last cooperative call: iteration 15, slots 4-9
+    auto stamp = [&](int k) {
+#ifdef QHUFF_PROFILE
+        if (pc)
+            prof_stamp(*pc, kProfIters - 1, k);
+#else
+        (void) k;
+        (void) pc;
+#endif
+    };
+    stamp(4);
     const uint32_t lane = lane_id();
     const bool mine = (coop >> lane) & 1;
     const uint32_t nb = mine ? 8 * (re - rs) : 0u;
@@ -727,6 +729,7 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
     seg_walk<kWalkMark>(src, E, stop, b1, s_win, s_sorted, bm, b0, nullptr,
                         nullptr, sink, C, h);
     wave_sync();
+    stamp(5);
     // B: walk on into the next segment of the string until meeting its marks
     const bool cl = act & (q + 1 < nsj);
     const uint32_t lim2 = !cl ? b1 : q + 2 < nsj ? s + 2 * S : b1;
@@ -751,6 +754,11 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
         if (++rounds > 64)                   // (cannot happen: segment q's
             return mine ? -1 : 0;            // exit is fixed after q rounds)
     }
+    stamp(6);
+#ifdef QHUFF_PROFILE
+    if (pc)
+        prof_value(*pc, kProfIters - 1, 9, rounds);
+#endif
     // symbols of each segment, offsets within the string
     const uint32_t kp = all_lanes(wave_shr1(K));
     const bool cnt_own = act && q >= 1 && pm;
@@ -764,6 +772,7 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
                                                    (int) (gj + nsj - 1), 64))
                      - base;
     const bool big = N > (8 * ((b1 - b0) >> 3)) / 5;   // more than the slot
+    stamp(7);
     // W: decode from the exact first symbol starts
     const uint32_t pcs = all_lanes(wave_shr1(cs));
     const uint32_t ts = q == 0 ? b0 : pcs;
@@ -772,6 +781,7 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
     seg_walk<kWalkEmit>(src, x, wr ? stop : b1, b1, s_win, s_sorted, bm, b0,
                         sl + (incl - T - base), sl + N, sink + 2 * lane, m,
                         bad);
+    stamp(8);
     // each exit must be the next segment's start
     const uint32_t nts = all_lanes((uint32_t) __shfl_down((int) ts, 1, 64));
     const bool chain = q + 1 < nsj ? x == nts : true;
@@ -888,7 +898,6 @@ compact_wave(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
 
 
 
-#if !QH_BIG_TILES
 // A tile whose input or output does not fit the stage, coded eagerly:
 // input staged -> the arena already holds the bytes (sz / st given);
 // otherwise count from global memory, then decode again to global.  The
@@ -899,7 +908,7 @@ compact_wave(const QH_LDS uint8_t *src, QH_LDS uint8_t *dstb, uint32_t n)
 // decoded before its error (DecPolicyT).
 template <bool Keep, class SM, class BaseOf>
 __device__ __noinline__ uint64_t
-dec_slow_tile_r3(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
+dec_slow_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
               uint32_t slot0, uint32_t cnt, TileOffs to, Span sp, uint32_t sz,
               uint32_t st, uint8_t *out, uint32_t *t_off, uint8_t *t_status,
               BaseOf base_of)
@@ -944,13 +953,12 @@ dec_slow_tile_r3(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
     return base + total;
 }
 
-#endif
 
-template <bool Keep, class SM, class BaseOf>
-__device__ __forceinline__ uint64_t
-dec_big_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv, uint32_t cnt,
-             TileOffs to, Span sp, uint32_t sz, uint32_t st, uint32_t slot0,
-             uint8_t *out, uint32_t *t_off, uint8_t *t_status, BaseOf base_of);
+template <bool Keep, class SM>
+__device__ __forceinline__ bool
+dec_big_sizes(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
+              uint32_t cnt, TileOffs to, Span sp, uint32_t &sz, uint32_t &st,
+              uint32_t slot0, uint8_t *dst);
 
 // the decode side of the wave pipeline (qhuff_pipeline.h, qhuff_service.hip);
 // SM: the workgroup's LDS (win, sorted).  Keep (the kernel the per-string
@@ -972,6 +980,9 @@ struct DecPolicyT
     QH_LDS DecWave *wv;
     uint32_t slot0;                  // this lane's arena slot (current tile)
     uint64_t coop = 0;               // strings decoded by the whole wave
+#ifdef QHUFF_PROFILE
+    const Coord *pc = nullptr;       // (profiling) stamps of coop_decode
+#endif
 
     __device__ __forceinline__ void stage_in(const Chunks<kNch> &ch,
                                              const Span &sp, const Offs &)
@@ -1037,7 +1048,11 @@ struct DecPolicyT
             const int rc = coop_decode(
                 wv->in, coop, rs, re, slot0, wv->arena,
                 (QH_LDS uint32_t *) (wv->arena + bm0),
-                wv->arena + kArenaBytes - kCoopDummy, sm->win, sm->sorted);
+                wv->arena + kArenaBytes - kCoopDummy, sm->win, sm->sorted
+#ifdef QHUFF_PROFILE
+                , pc
+#endif
+                );
             r = mine ? rc : r;
             const uint64_t fail = __builtin_amdgcn_ballot_w64(mine & (rc < 0));
 #ifdef QH_COOP_DEBUG
@@ -1098,23 +1113,26 @@ struct DecPolicyT
     }
 
     // a tile of the batch kernel: base from the look-back
-    template <class BaseOf>
+    // a big tile's sizes, and its output into dst when it fits
+    __device__ __forceinline__ bool big_sizes(uint32_t cnt, Offs to, Span sp,
+                                              uint32_t &sz, uint32_t &st,
+                                              uint8_t *dst)
+    {
+        return dec_big_sizes<Keep>(in, sm, wv, cnt, to, sp, sz, st, slot0, dst);
+    }
+    // a big tile whose output does not fit a slot (qhuff_pipeline.h), after
+    // the pending tiles are flushed: base from the look-back
     __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
                                               Offs to, Span sp, uint32_t sz,
                                               uint32_t st, uint8_t *out,
                                               uint32_t *out_off, uint8_t *status,
-                                              uint64_t n, BaseOf base_of)
+                                              uint64_t n)
     {
         const uint64_t s0 = (uint64_t) t * kTS;
-#if QH_BIG_TILES
-        const uint64_t end = dec_big_tile<Keep>(in, sm, wv, cnt, to, sp, sz, st,
-                                                slot0, out, out_off + s0,
-                                                status + s0, base_of);
-#else
-        const uint64_t end = dec_slow_tile_r3<Keep>(in, sm, wv, slot0, cnt, to,
+        const uint64_t end = dec_slow_tile<Keep>(in, sm, wv, slot0, cnt, to,
                                                     sp, sz, st, out, out_off + s0,
-                                                    status + s0, base_of);
-#endif
+                                                    status + s0,
+                                                    LookBackBase{c, t});
         last_tile_end(c, t, end, out_off, n);
     }
     // a tile at a known base
@@ -1124,191 +1142,118 @@ struct DecPolicyT
                                                      uint32_t *t_off,
                                                      uint8_t *t_status)
     {
-#if QH_BIG_TILES
-        return dec_big_tile<Keep>(in, sm, wv, cnt, to, sp, sz, st, slot0, out,
-                                  t_off, t_status, FixedBase{base});
-#else
-        return dec_slow_tile_r3<Keep>(in, sm, wv, slot0, cnt, to, sp, sz, st,
+        return dec_slow_tile<Keep>(in, sm, wv, slot0, cnt, to, sp, sz, st,
                                       out, t_off, t_status, FixedBase{base});
-#endif
     }
 };
 
-// A tile whose input or output does not fit the stages, coded eagerly
-// in units -- runs of its strings whose input (and output) fit the
-// stages: each staged and decoded like a fast tile.  Sizes first (unit
-// by unit; given when the whole input was staged), then the base
-// (base_of: the batch kernel's look-back, or the service's running
-// offset), then every unit again, compacted and stored.  A string whose
-// input alone exceeds the stage is walked in global memory by its lane;
-// one whose output alone exceeds it is decoded in the arena and copied
-// out by the wave.  Offsets and statuses go to t_off / t_status (the
-// tile's first string).  Returns base + total.  Out of line (cold).
-// (A free function with its own policy object: a member called out of
-// line would take the address of the pipeline's policy, and the kernel's
-// hot loop would then keep its fields in scratch memory.)
-template <bool Keep, class SM, class BaseOf>
-__device__ __forceinline__ uint64_t
-dec_big_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
-             uint32_t cnt, TileOffs to, Span sp, uint32_t sz, uint32_t st,
-             uint32_t slot0, uint8_t *out, uint32_t *t_off, uint8_t *t_status,
-             BaseOf base_of)
+
+// The sizes of a big tile (statuses too) and, when they fit kBigSlotBytes,
+// its whole compacted output at dst (a big-tile slot, qhuff_pipeline.h),
+// written before its base is known: the tile then waits for its look-back
+// like any other, and its wave goes on coding.  Staged input: the main
+// codec has sized and decoded it into the arena (sz, st, slot0 given).
+// Otherwise unit by unit, each staged, decoded into the arena and copied
+// from there; a string whose input alone exceeds the stage is walked in
+// global memory (into dst when its bound fits).  Returns whether all of
+// the output went to dst; the sizes are complete either way.
+template <bool Keep, class SM>
+__device__ __forceinline__ bool
+dec_big_sizes(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
+              uint32_t cnt, TileOffs to, Span sp, uint32_t &sz, uint32_t &st,
+              uint32_t slot0, uint8_t *dst)
 {
     using P = DecPolicyT<SM, Keep>;
-    constexpr int kInCap = P::kInCap, kOutCap = P::kOutCap, kNch = P::kNch;
     P pol{in, sm, wv, 0};
     const uint32_t lane = lane_id();
-    const bool valid = lane < cnt;
-    auto stage = [&](uint32_t i0, uint32_t i1) -> Span {
-        const Span su = tile_span(in, read_lane(to.o0, i0),
-                                  read_lane(to.o1, i1 - 1), kInCap);
-        stage_chunks<true>(su, (QH_LDS u32x4 *) wv->in);
-        return su;
-    };
-    // a string beyond the stage, in global memory
-    auto glb = [&](uint32_t i, uint8_t *dst, uint32_t *n) -> int {
-        const uintptr_t pa = (uintptr_t) (in + read_lane(to.o0, i))
-                           & ~(uintptr_t) 15;
-        const DecGlb src{(const QH_GLB uint32_t *) pa};
-        const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - pa);
-        const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - pa);
-        int r = 0;
-        if (lane == i)
+    uint32_t run = 0;                        // output bytes so far (uniform)
+    bool fits = true;
+    // the arena slots of lanes [lo, hi) -> dst + run, compacted
+    auto put = [&](uint32_t lo, uint32_t hi, uint32_t s, uint32_t t,
+                   uint32_t slot) {
+        const bool in_u = (lane >= lo) & (lane < hi);
+        const uint32_t ls = in_u & (Keep || t == QHUFF_DEC_OK) ? s : 0u;
+        const uint32_t incl = all_lanes(wave_incl_scan(ls));
+        const uint32_t ut = read_lane(incl, 63);
+        fits = fits && run + ut <= kBigSlotBytes;
+        if (fits)
         {
-            if (dst)
+            const bool lng = ls > 64;
+            if (ls && !lng)
             {
-                GlobalEmit em{dst, 0};
-                r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted,
-                                  em);
+                const QH_LDS uint8_t *sa = wv->arena + slot;
+                uint8_t *d = dst + run + (incl - ls);
+                for (uint32_t i = 0; i < ls; ++i)
+                    ((QH_GLB uint8_t *) d)[i] = sa[i];
             }
-            else
+            for (uint64_t m = __builtin_amdgcn_ballot_w64(lng); m; m &= m - 1)
             {
-                CountEmit em{0};
-                r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted,
-                                  em);
+                const uint32_t j = (uint32_t) __builtin_ctzll(m);
+                copy_out(wv->arena + read_lane(slot, j),
+                         dst + run + read_lane(incl - ls, j), read_lane(ls, j));
             }
         }
-        (void) n;
-        return r;
+        run += ut;
     };
-#ifdef QH_SKIP_SLOW
-    // (timing experiments only: big tiles coded as empty -- wrong output)
+    if (sp.staged)
     {
-        const uint64_t b0 = base_of(0);
-        if (valid)
-            ((QH_GLB uint32_t *) t_off)[lane] = (uint32_t) b0;
-        return b0;
+        put(0, cnt, sz, st, slot0);
+        return fits;
     }
-#endif
-    // sizes
-    if (!sp.staged)
+    sz = 0;
+    st = 0;
+    for (uint32_t i0 = 0; i0 < cnt;)
     {
-        sz = 0;
-        st = 0;
-        for (uint32_t i0 = 0; i0 < cnt;)
+        const uint32_t k = unit_len(in, to, i0, cnt, P::kInCap, false, 0, 0, 0);
+        if (k == 0)
         {
-            const uint32_t k = unit_len(in, to, i0, cnt, kInCap, false, 0,
-                                        0, 0);
+            // one string beyond the stage: its lane walks it in global memory
+            const uintptr_t pa = (uintptr_t) (in + read_lane(to.o0, i0))
+                               & ~(uintptr_t) 15;
+            const DecGlb src{(const QH_GLB uint32_t *) pa};
+            const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - pa);
+            const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - pa);
+            const uint32_t bound = (8 * read_lane(re - rs, i0)) / 5 + 1;
+            const bool w = fits && run + bound <= kBigSlotBytes;
             int r = 0;
-            if (k == 0)
+            if (lane == i0)
             {
-                r = glb(i0, nullptr, nullptr);
-                if (lane != i0)
-                    r = 0;
-            }
-            else
-            {
-                const Span su = stage(i0, i0 + k);
-                uint32_t s1, t1;
-                pol.codec_range(to, i0, i0 + k, su, &s1, &t1);
-                r = t1 == QHUFF_DEC_OK ? (int) s1
-                                       : -1 - (Keep ? (int) s1 : 0);
-                wave_sync();
-            }
-            const uint32_t kk = k ? k : 1u;
-            const bool in_u = (lane >= i0) & (lane < i0 + kk);
-            if (in_u)
-            {
+                if (w)
+                {
+                    GlobalEmit em{dst + run, 0};
+                    r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted,
+                                      em);
+                }
+                else
+                {
+                    CountEmit em{0};
+                    r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted,
+                                      em);
+                }
                 sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
                 st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
             }
-            i0 += kk;
-        }
-    }
-    sz = valid ? sz : 0u;
-    const uint32_t incl = wave_incl_scan(sz);
-    const uint32_t excl = incl - sz;
-    const uint32_t total = read_lane(incl, 63);
-    const uint64_t base = base_of(total);
-    if (sp.staged)
-    {
-        // the tile was decoded whole into the arena (slot0): only its
-        // output overflows the stage -- copied out from there, the long
-        // strings by the whole wave, the others by their lanes
-        const bool lng = valid & (sz > 64);
-        if (valid && !lng && (Keep || st == QHUFF_DEC_OK))
-        {
-            const QH_LDS uint8_t *sa = wv->arena + slot0;
-            uint8_t *d = out + base + excl;
-            for (uint32_t i = 0; i < sz; ++i)
-                ((QH_GLB uint8_t *) d)[i] = sa[i];
-        }
-        for (uint64_t m = __builtin_amdgcn_ballot_w64(lng); m; m &= m - 1)
-        {
-            const uint32_t j = (uint32_t) __builtin_ctzll(m);
-            copy_out(wv->arena + read_lane(slot0, j),
-                     out + base + read_lane(excl, j), read_lane(sz, j));
-        }
-    }
-    // outputs, unit by unit
-    for (uint32_t i0 = 0; i0 < (sp.staged ? 0u : cnt);)
-    {
-        const uint32_t k = unit_len(in, to, i0, cnt, kInCap, true, excl, sz,
-                                    kOutCap);
-        const uint32_t e0 = read_lane(excl, i0);
-        if (k == 0)
-        {
-            // one string: input beyond the stage -> global walk; output
-            // beyond it -> the arena, copied out by the wave
-            const uint32_t si = read_lane(sz, i0);
-            const uint32_t sti = read_lane(st, i0);
-            if (unit_len(in, to, i0, cnt, kInCap, false, 0, 0, 0) == 0)
-            {
-                if (si && (Keep || sti == QHUFF_DEC_OK))
-                    glb(i0, out + base + e0, nullptr);
-            }
-            else if (si && (Keep || sti == QHUFF_DEC_OK))
-            {
-                const Span su = stage(i0, i0 + 1);
-                uint32_t s1, t1;
-                pol.codec_range(to, i0, i0 + 1, su, &s1, &t1);
-                wave_sync();
-                copy_out(wv->arena + read_lane(pol.slot0, i0), out + base + e0,
-                         si);
-            }
-            wave_sync();
+            fits = w;
+            run += read_lane(sz, i0);
             i0 += 1;
             continue;
         }
-        const uint32_t i1 = i0 + k;
-        const Span su = stage(i0, i1);
+        const Span su = tile_span(in, read_lane(to.o0, i0),
+                                  read_lane(to.o1, i0 + k - 1), P::kInCap);
+        stage_chunks<true>(su, (QH_LDS u32x4 *) wv->in);
         uint32_t s1, t1;
-        pol.codec_range(to, i0, i1, su, &s1, &t1);
-        const bool in_u = (lane >= i0) & (lane < i1);
-        const uint32_t ul = read_lane(incl, i1 - 1) - e0;
+        pol.codec_range(to, i0, i0 + k, su, &s1, &t1);
         wave_sync();
-        pol.emit(in_u ? excl - e0 : 0u, in_u ? s1 : 0u, ul);
+        put(i0, i0 + k, s1, t1, pol.slot0);
+        if ((lane >= i0) & (lane < i0 + k))
+        {
+            sz = s1;
+            st = t1;
+        }
         wave_sync();
-        copy_out((const QH_LDS uint8_t *) wv->in, out + base + e0, ul);
-        wave_sync();
-        i0 = i1;
+        i0 += k;
     }
-    if (valid)
-    {
-        ((QH_GLB uint32_t *) t_off)[lane] = (uint32_t) (base + excl);
-        ((QH_GLB uint8_t *) t_status)[lane] = (uint8_t) st;
-    }
-    return base + total;
+    return fits;
 }
 
 }  // namespace qhuff

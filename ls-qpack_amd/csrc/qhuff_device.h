@@ -95,7 +95,18 @@ struct Coord
                                             // each workgroup take one tile
                                             // each from counter 0 (batches
                                             // the grid covers; qhuff_pipeline.h)
+    uint8_t *big;                           // big-tile output slots:
+                                            // kBigSlots per wave of the grid
 };
+
+// A big tile's output (qhuff_pipeline.h) waits in one of its wave's
+// kBigSlots global slots of kBigSlotBytes until the tile is flushed: as
+// many slots as pending tiles + 1 (the tile coded in an iteration is placed
+// before that iteration's flush frees the oldest).
+constexpr uint32_t kBigSlots = 4;
+constexpr uint32_t kBigSlotBytes = 12288;
+constexpr uint32_t kBigMaxWaves = 16;       // per workgroup (host allocation)
+static_assert(kWaves <= (int) kBigMaxWaves, "big-tile slots per workgroup");
 
 struct Coord;
 __device__ __forceinline__ void raise_error(const Coord &c, uint32_t bits);

@@ -696,7 +696,6 @@ emit_dense(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
     return p0;
 }
 
-#if !QH_BIG_TILES
 // A tile whose input or output does not fit the stages, coded eagerly:
 // sizes from the stage (given) or from global memory, then packed straight
 // to global memory.  The tile's output base comes from base_of(total) (the
@@ -705,7 +704,7 @@ emit_dense(const QH_LDS uint32_t *in, uint32_t rs, uint32_t re, uint32_t mode,
 // (cold), state by value.
 template <class SM, class BaseOf>
 __device__ __noinline__ uint64_t
-enc_slow_tile_r3(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
+enc_slow_tile(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
               QH_LDS EncWave *wv, uint32_t rs, uint32_t re, EncSize z,
               uint32_t cnt, TileOffs to, Span sp, uint32_t sz, uint8_t *out,
               uint32_t *t_off, BaseOf base_of)
@@ -744,13 +743,12 @@ enc_slow_tile_r3(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
     return base + total;
 }
 
-#endif
 
-template <class SM, class BaseOf>
-__device__ __forceinline__ uint64_t
-enc_big_tile(const uint8_t *in, uint32_t mode, QH_LDS SM *sm, QH_LDS EncWave *wv,
-             uint32_t cnt, TileOffs to, Span sp, uint32_t sz, uint8_t *out,
-             uint32_t *t_off, BaseOf base_of);
+template <class SM>
+__device__ __forceinline__ bool
+enc_big_sizes(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
+              QH_LDS EncWave *wv, uint32_t cnt, TileOffs to, Span sp,
+              uint32_t &sz, uint8_t *dst);
 
 // the encode side of the wave pipeline (qhuff_pipeline.h, qhuff_service.hip);
 // SM: the workgroup's LDS (enc, mt, len)
@@ -879,23 +877,26 @@ struct EncPolicyT
     }
 
     // a tile of the batch kernel: base from the look-back
-    template <class BaseOf>
+    // a big tile's sizes, and its output into dst when it fits
+    __device__ __forceinline__ bool big_sizes(uint32_t cnt, TileOffs to, Span sp,
+                                              uint32_t &sz, uint32_t &st,
+                                              uint8_t *dst)
+    {
+        st = 0;
+        return enc_big_sizes(in, mode, sm, wv, cnt, to, sp, sz, dst);
+    }
+    // a big tile whose output does not fit a slot (qhuff_pipeline.h), after
+    // the pending tiles are flushed: base from the look-back
     __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
                                               TileOffs to, Span sp, uint32_t sz,
                                               uint32_t, uint8_t *out,
                                               uint32_t *out_off, uint8_t *,
-                                              uint64_t n, BaseOf base_of)
+                                              uint64_t n)
     {
-#if QH_BIG_TILES
-        const uint64_t end = enc_big_tile(in, mode, sm, wv, cnt, to, sp, sz,
-                                          out, out_off + (uint64_t) t * kTS,
-                                          base_of);
-#else
-        const uint64_t end = enc_slow_tile_r3(in, mode, sm, wv, rs, re, z, cnt,
+        const uint64_t end = enc_slow_tile(in, mode, sm, wv, rs, re, z, cnt,
                                               to, sp, sz, out,
                                               out_off + (uint64_t) t * kTS,
-                                              base_of);
-#endif
+                                              LookBackBase{c, t});
         last_tile_end(c, t, end, out_off, n);
     }
     // a tile at a known base
@@ -905,160 +906,122 @@ struct EncPolicyT
                                                      uint8_t *out, uint32_t *t_off,
                                                      uint8_t *)
     {
-#if QH_BIG_TILES
-        return enc_big_tile(in, mode, sm, wv, cnt, to, sp, sz, out, t_off,
-                            FixedBase{base});
-#else
-        return enc_slow_tile_r3(in, mode, sm, wv, rs, re, z, cnt, to, sp, sz,
+        return enc_slow_tile(in, mode, sm, wv, rs, re, z, cnt, to, sp, sz,
                                 out, t_off, FixedBase{base});
-#endif
     }
 };
 
-// A tile whose input or output does not fit the stages, coded eagerly in
-// units -- runs of its strings whose input (and output) fit the stages,
-// each staged, dense-passed and sized like a fast tile: sizes first (unit by
-// unit; given when the whole input was staged), then the base (base_of: the
-// batch kernel's look-back, or the service's running offset), then every
-// unit again, packed into the out stage and stored.  A string whose input
-// alone exceeds the stage is sized and packed from global memory by its
-// lane; one whose output alone exceeds the out stage is packed from the
-// staged input straight to global memory.  Offsets go to t_off (the tile's
-// first string).  Returns base + total.  (Inline, in the cold branch: an
-// out-of-line call with the codec inside made the kernel's hot loop spill.)
-template <class SM, class BaseOf>
-__device__ __forceinline__ uint64_t
-enc_big_tile(const uint8_t *in, uint32_t mode, QH_LDS SM *sm, QH_LDS EncWave *wv,
-             uint32_t cnt, TileOffs to, Span sp, uint32_t sz, uint8_t *out,
-             uint32_t *t_off, BaseOf base_of)
+
+// The sizes of a big tile and, when they fit kBigSlotBytes, its whole
+// packed output at dst (a big-tile slot, qhuff_pipeline.h), written before
+// its base is known.  Staged input (sizes given by the main codec): packed
+// by each lane from the stage.  Otherwise unit by unit, each staged,
+// dense-passed, sized and packed into the out stage (or, past it, by each
+// lane); a string whose input alone exceeds the stage is sized and packed
+// from global memory by its lane.  Returns whether all of the output went to
+// dst; the sizes are complete either way.
+template <class SM>
+__device__ __forceinline__ bool
+enc_big_sizes(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
+              QH_LDS EncWave *wv, uint32_t cnt, TileOffs to, Span sp,
+              uint32_t &sz, uint8_t *dst)
 {
     using P = EncPolicyT<SM>;
     P pol{in, mode, sm, wv};
     const uint32_t lane = lane_id();
     const bool valid = lane < cnt;
-    auto stage = [&](uint32_t i0, uint32_t i1) -> Span {
+    // per-lane packing of lanes [lo, hi) from the LDS stage (span su) at
+    // dst + at (this lane's offset)
+    auto pack_lds = [&](uint32_t lo, uint32_t hi, const Span &su, uint32_t at) {
+        if ((lane >= lo) & (lane < hi))
+        {
+            const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - su.pa);
+            const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - su.pa);
+            const EncSize z = size_string(mode, EncLds{wv->in}, rs, re, sm->len);
+            if (z.size)
+            {
+                Packer<PackGlb> pk;
+                pk.sink.out = dst;
+                pk.init(at, at + z.size);
+                emit_string(EncLds{wv->in}, rs, re, mode, z.huff, z.plen,
+                            sm->enc, pk);
+            }
+        }
+    };
+    if (sp.staged)
+    {
+        const uint32_t s = valid ? sz : 0u;
+        const uint32_t incl = all_lanes(wave_incl_scan(s));
+        if (read_lane(incl, 63) > kBigSlotBytes)
+            return false;
+        pack_lds(0, cnt, sp, incl - s);
+        return true;
+    }
+    uint32_t run = 0;
+    bool fits = true;
+    sz = 0;
+    for (uint32_t i0 = 0; i0 < cnt;)
+    {
+        const uint32_t k = unit_len(in, to, i0, cnt, P::kInCap, false, 0, 0, 0);
+        if (k == 0)
+        {
+            // one string beyond the stage, from global memory by its lane
+            const uintptr_t pa = (uintptr_t) (in + read_lane(to.o0, i0))
+                               & ~(uintptr_t) 15;
+            const EncGlb src{(const QH_GLB uint32_t *) pa};
+            const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - pa);
+            const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - pa);
+            EncSize z = (EncSize){0, 0, true};
+            if (lane == i0)
+            {
+                z = size_string(mode, src, rs, re, sm->len);
+                sz = z.size;
+            }
+            const uint32_t n = read_lane(sz, i0);
+            fits = fits && run + n <= kBigSlotBytes;
+            if (fits && lane == i0 && n)
+            {
+                Packer<PackGlb> pk;
+                pk.sink.out = dst;
+                pk.init(run, run + n);
+                emit_string(src, rs, re, mode, z.huff, z.plen, sm->enc, pk);
+            }
+            run += n;
+            i0 += 1;
+            continue;
+        }
+        const uint32_t i1 = i0 + k;
         const Span su = tile_span(in, read_lane(to.o0, i0),
                                   read_lane(to.o1, i1 - 1), P::kInCap);
         stage_chunks<false>(su, (QH_LDS u32x4 *) wv->in);
         pol.prepare(su);
         wave_sync();
-        return su;
-    };
-    // string i from global memory: its size, or (dst) its packed bytes
-    auto glb = [&](uint32_t i, bool pack, uint64_t at) -> uint32_t {
-        const uintptr_t pa = (uintptr_t) (in + read_lane(to.o0, i))
-                           & ~(uintptr_t) 15;
-        const EncGlb src{(const QH_GLB uint32_t *) pa};
-        const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - pa);
-        const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - pa);
-        uint32_t n = 0;
-        if (lane == i)
-        {
-            const EncSize z = size_string(mode, src, rs, re, sm->len);
-            n = z.size;
-            if (pack && n)
-            {
-                const uint32_t adj = (uint32_t) ((uintptr_t) out & 3);
-                Packer<PackGlb> pk;
-                pk.sink.out = out - adj;
-                const uint32_t p0 = adj + (uint32_t) at;
-                pk.init(p0, p0 + n);
-                emit_string(src, rs, re, mode, z.huff, z.plen, sm->enc, pk);
-            }
-        }
-        return n;
-    };
-#ifdef QH_SKIP_SLOW
-    // (timing experiments only: big tiles coded as empty -- wrong output)
-    {
-        const uint64_t b0 = base_of(0);
-        if (valid)
-            ((QH_GLB uint32_t *) t_off)[lane] = (uint32_t) b0;
-        return b0;
-    }
-#endif
-    if (!sp.staged)
-    {
-        sz = 0;
-        for (uint32_t i0 = 0; i0 < cnt;)
-        {
-            const uint32_t k = unit_len(in, to, i0, cnt, P::kInCap, false, 0, 0,
-                                        0);
-            uint32_t n = 0;
-            if (k == 0)
-                n = glb(i0, false, 0);
-            else
-            {
-                const Span su = stage(i0, i0 + k);
-                uint32_t s1, t1;
-                pol.codec_range(to, i0, i0 + k, su, &s1, &t1);
-                n = s1;
-                wave_sync();
-            }
-            const uint32_t kk = k ? k : 1u;
-            if ((lane >= i0) & (lane < i0 + kk))
-                sz = n;
-            i0 += kk;
-        }
-    }
-    sz = valid ? sz : 0u;
-    const uint32_t incl = wave_incl_scan(sz);
-    const uint32_t excl = incl - sz;
-    const uint32_t total = read_lane(incl, 63);
-    const uint64_t base = base_of(total);
-    for (uint32_t i0 = 0; i0 < cnt;)
-    {
-        const uint32_t k = unit_len(in, to, i0, cnt, P::kInCap, true, excl, sz,
-                                    P::kOutCap);
-        const uint32_t e0 = read_lane(excl, i0);
-        if (k == 0)
-        {
-            if (read_lane(sz, i0))
-            {
-                if (unit_len(in, to, i0, cnt, P::kInCap, false, 0, 0, 0) == 0)
-                    glb(i0, true, base + e0);
-                else
-                {
-                    // output beyond the out stage: packed from the stage
-                    const Span su = stage(i0, i0 + 1);
-                    const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0)
-                                                    - su.pa);
-                    const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1)
-                                                    - su.pa);
-                    if (lane == i0)
-                    {
-                        const EncSize z = size_string(mode, EncLds{wv->in}, rs,
-                                                      re, sm->len);
-                        const uint32_t adj = (uint32_t) ((uintptr_t) out & 3);
-                        Packer<PackGlb> pk;
-                        pk.sink.out = out - adj;
-                        const uint32_t p0 = adj + (uint32_t) (base + e0);
-                        pk.init(p0, p0 + z.size);
-                        emit_string(EncLds{wv->in}, rs, re, mode, z.huff,
-                                    z.plen, sm->enc, pk);
-                    }
-                }
-            }
-            wave_sync();
-            i0 += 1;
-            continue;
-        }
-        const uint32_t i1 = i0 + k;
-        const Span su = stage(i0, i1);
         uint32_t s1, t1;
         pol.codec_range(to, i0, i1, su, &s1, &t1);
         const bool in_u = (lane >= i0) & (lane < i1);
-        const uint32_t ul = read_lane(incl, i1 - 1) - e0;
-        wave_sync();
-        pol.emit(in_u ? excl - e0 : 0u, in_u ? s1 : 0u, ul);
-        wave_sync();
-        copy_out((const QH_LDS uint8_t *) wv->out, out + base + e0, ul);
+        const uint32_t ls = in_u ? s1 : 0u;
+        const uint32_t incl = all_lanes(wave_incl_scan(ls));
+        const uint32_t ut = read_lane(incl, 63);
+        fits = fits && run + ut <= kBigSlotBytes;
+        if (fits)
+        {
+            if (ut + 64 <= (uint32_t) P::kOutCap)
+            {
+                wave_sync();
+                pol.emit(in_u ? incl - ls : 0u, ls, ut);
+                wave_sync();
+                copy_out((const QH_LDS uint8_t *) wv->out, dst + run, ut);
+            }
+            else
+                pack_lds(i0, i1, su, run + incl - ls);
+        }
+        if (in_u)
+            sz = s1;
+        run += ut;
         wave_sync();
         i0 = i1;
     }
-    if (valid)
-        ((QH_GLB uint32_t *) t_off)[lane] = (uint32_t) (base + excl);
-    return base + total;
+    return fits;
 }
 
 // the code tables, loaded once per workgroup (threads 0..256)

@@ -152,6 +152,8 @@ struct qhuff_ctx
     uint32_t *err;                       // device: [0] error word, [1..3]
                                          // census, then claim counters
     uint64_t cap_tiles, cap_super;
+    uint8_t *big;                        // device: big-tile output slots
+                                         // (Coord::big), kBigSlots per wave
     unsigned long long *prof;            // QHUFF_PROFILE builds: stamp buffer
     size_t prof_words;
     uint32_t epoch;
@@ -280,6 +282,15 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     if (e == hipSuccess)
         e = hipMemset(c->err, 0, kErrWords * sizeof(uint32_t));
     if (e == hipSuccess)
+    {
+        // kBigSlots output slots per wave of the larger grid (192 MB on
+        // 256 CUs): big tiles (qhuff_pipeline.h)
+        const uint64_t waves = (uint64_t) (c->enc_grid > c->dec_grid
+                                           ? c->enc_grid : c->dec_grid)
+                             * kBigMaxWaves;
+        e = hipMalloc((void **) &c->big, waves * kBigSlots * kBigSlotBytes);
+    }
+    if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming);
@@ -341,6 +352,8 @@ qhuff_close(qhuff_ctx *c)
         (void) hipFree(c->tab);
     if (c->flags)
         (void) hipFree(c->flags);
+    if (c->big)
+        (void) hipFree(c->big);
     if (c->err)
         (void) hipFree(c->err);
     if (c->d_stage)
@@ -527,6 +540,7 @@ coord(qhuff_ctx *c, uint64_t tiles)
     k.epoch = c->epoch;
     k.n_tiles = (uint32_t) tiles;
     k.spread = 0;
+    k.big = c->big;
     return k;
 }
 

@@ -39,10 +39,10 @@
 
 #include "qhuff_kernels.h"
 
-// Big tiles (input or output past the stages) coded in staged units,
-// inline, their aggregate published before the pending tiles are flushed
-// (qhuff_*_impl.h *_big_tile); 0: the round-3 path, an out-of-line per-lane
-// walk over global memory after the pending tiles are flushed.
+// Big tiles (input or output past the stages) sized in staged units and
+// their output written to a per-wave slot, then pending like any other tile
+// (qhuff_*_impl.h *_big_sizes); 0: the round-3 path only, an out-of-line
+// per-lane walk over global memory after the pending tiles are flushed.
 #ifndef QH_BIG_TILES
 #define QH_BIG_TILES 1
 #endif
@@ -62,6 +62,8 @@ struct Pending
     uint32_t excl;                   // this lane's tile-local output offset
     uint32_t stat;                   // this lane's status byte
     uint32_t tile, total;            // (wave-uniform)
+    uint32_t big;                    // (wave-uniform) a big tile: 1 + its
+                                     // output slot; 0: output in TileOut
     __device__ __forceinline__ LookBack lb() const
     {
         LookBack l;
@@ -69,6 +71,17 @@ struct Pending
         return l;
     }
 };
+
+// A cross-lane result (DPP, ds_bpermute), computed by every lane here: left
+// to itself the compiler may move the operation into the branch of a select
+// that uses it, where the lanes it reads from are off (and read as 0).
+template <class T>
+__device__ __forceinline__ T
+all_lanes(T v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 // Output base of a slow tile (P::slow_tile / slow_tile_at): the batch
 // kernel's look-back, or a base the caller already has (the service kernel
@@ -173,6 +186,36 @@ stage_chunks(const Span &sp, QH_LDS u32x4 *dst)
     wave_sync();
 }
 
+// this wave's big-tile output slot k (Coord::big)
+__device__ __forceinline__ uint8_t *
+big_slot(const Coord &c, uint32_t k)
+{
+    const uint64_t gid = (uint64_t) blockIdx.x * kWaves + (threadIdx.x >> 6);
+    return c.big + (gid * kBigSlots + k) * (uint64_t) kBigSlotBytes;
+}
+
+// n bytes of a big-tile slot -> dst (any alignment), the whole wave.  The
+// slot was written by this wave a few iterations ago and is read back
+// through L2 (agent-scope loads): an earlier read of the same slot may
+// still sit in this CU's L1.
+__device__ __forceinline__ void
+copy_slot(const uint8_t *src, uint8_t *dst, uint32_t n)
+{
+    const uint32_t lane = lane_id();
+    const QH_GLB uint32_t *s = (const QH_GLB uint32_t *) src;
+    auto ld = [&](uint32_t w) -> uint32_t {
+        return __hip_atomic_load(s + w, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    };
+    const uint32_t n16 = n >> 4;
+    for (uint32_t i = lane; i < n16; i += 64)
+        ((QH_GLB U4 *) (dst + 16 * i))->v =
+            (u32x4){ld(4 * i), ld(4 * i + 1), ld(4 * i + 2), ld(4 * i + 3)};
+    const uint32_t t = 16 * n16 + lane;
+    if (lane < 16 && t < n)
+        ((QH_GLB uint8_t *) dst)[t] = (uint8_t) (ld(t >> 2) >> (8 * (t & 3)));
+}
+
 // resolve a pending tile's base and store it from `o` (every lane)
 template <class P>
 __device__ __forceinline__ void
@@ -189,7 +232,10 @@ flush_tile(const Coord &c, Pending &d, LookBack &lb, const TileOut<P::kNch> &o,
     // live in SGPRs)
     const uint32_t tile = __builtin_amdgcn_readfirstlane(d.tile);
     const uint32_t total = d.total;
-    o.store(out + base, total);
+    if (__builtin_expect(d.big != 0, 0))
+        copy_slot(big_slot(c, d.big - 1), out + base, total);
+    else
+        o.store(out + base, total);
     uint32_t lane = lane_id();
     // (opaque: the per-lane addresses are rebuilt here, not hoisted out of
     // the tile loop as a register pair each)
@@ -418,7 +464,11 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     };
 #pragma unroll
     for (int i = 0; i < D; ++i)
+    {
         pend[i].valid = false;
+        pend[i].big = 0;
+    }
+    uint32_t big_next = 0;                   // big-tile slots used (ring)
     uint32_t it = 0;
     for (;; ++it)
     {
@@ -476,16 +526,57 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
             pol.prepare(sp_cur);
             pol.codec(o_cur, cnt, sp_cur, &sz, &st);
         }
-        const uint32_t incl = wave_incl_scan(sz);
-        const uint32_t excl = incl - sz;
-        const uint32_t total = read_lane(incl, 63);
+        uint32_t incl = wave_incl_scan(sz);
+        uint32_t excl = incl - sz;
+        uint32_t total = read_lane(incl, 63);
         fast = fast && total + 64 <= (uint32_t) P::kOutCap;
+#if QH_BIG_TILES
+        // A big tile (input or output past the stages): its sizes, in
+        // staged units, and its output into one of the wave's big-tile slots
+        // (P::big_sizes).  When it fits, it is pending like any other tile
+        // from here on -- its output copied from the slot when its look-back
+        // resolves -- and the wave goes straight on to its next tile.
+        uint32_t bigslot = 0;                // (wave-uniform) 1 + the slot
+        if (!fast)
+        {
+            // the pending tiles' outputs move to slots first, so that their
+            // registers are free for the big tile's codec (the slots hold
+            // every tile in flight: kDepth pending + this one)
+#pragma unroll
+            for (int i = 0; i < D; ++i)
+            {
+                if (pend[i].valid && !pend[i].big)
+                {
+                    const uint32_t kp = big_next % kBigSlots;
+                    ++big_next;
+                    outs[i].store(big_slot(c, kp), pend[i].total);
+                    pend[i].big = kp + 1;
+                }
+                outs[i].clear();
+            }
+            const uint32_t k = big_next % kBigSlots;
+            if (pol.big_sizes(cnt, o_cur, sp_cur, sz, st, big_slot(c, k)))
+            {
+                bigslot = k + 1;
+                ++big_next;
+            }
+            incl = wave_incl_scan(sz);
+            excl = incl - sz;
+            total = read_lane(incl, 63);
+            // the next tile's input again: its chunk registers were free
+            // through the big tile's codec
+            ch.load(sp_nxt);
+        }
+#else
+        constexpr uint32_t bigslot = 0;
+#endif
         prof_stamp(c, it, 3);
 
         Pending cur;
         cur.valid = false;
+        cur.big = 0;
         LookBack lbc;                        // t's publication
-        if (fast)
+        if (fast || bigslot)
         {
             // publish t's aggregate, pack t into the LDS out stage
             cur.valid = true;
@@ -493,10 +584,14 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
             cur.stat = st;
             cur.tile = t;
             cur.total = total;
+            cur.big = bigslot;
             lbc.start(c, t, total);
-            wave_sync();
-            pol.emit(excl, sz, total);
-            wave_sync();
+            if (fast)
+            {
+                wave_sync();
+                pol.emit(excl, sz, total);
+                wave_sync();
+            }
         }
         prof_stamp(c, it, 9);
 #ifdef QHUFF_PROFILE
@@ -536,48 +631,14 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
 
         if (fast)
             outs[D - 1].gather(pol.out_stage());
-#if QH_BIG_TILES
+        else if (bigslot)
+            outs[D - 1].clear();             // (its output is in its slot)
         else
         {
-            // A big tile (P::slow_tile: sizes, then the base, then the
-            // output).  Its aggregate is published as soon as its sizes are
-            // known, and only then are the pending tiles flushed: a flush
-            // waits on earlier tiles, other big tiles among them, so flushing
-            // first would chain the big tiles of the batch one after another.
-            auto base_of = [&](uint32_t total) -> uint64_t {
-                prof_stamp(c, kProfIters - 1, 1);
-                LookBack lb;
-                lb.start(c, t, total);
-#pragma unroll
-                for (int i = 0; i < D; ++i)
-                    if (pend[i].valid)
-                    {
-                        LookBack l = pend[i].lb();
-                        l.poll(c);
-                        flush_at(i, l, ~0u);
-                    }
-                // the flushed outputs are dead: constants in their registers
-                // (rematerialised, not kept) leave them to the output pass
-#pragma unroll
-                for (int i = 0; i < D; ++i)
-                    outs[i].clear();
-                lb.super_agg(c);
-                lb.poll(c);
-                const uint64_t b = lb.finish(c);
-                prof_stamp(c, kProfIters - 1, 2);
-                return b;
-            };
-            prof_stamp(c, kProfIters - 1, 0);    // (profiling) big tile
-            pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
-                          status, n, base_of);
-            prof_stamp(c, kProfIters - 1, 3);
-        }
-#else
-        else
-        {
-            // (a slow tile only needs its predecessors' aggregates; the
-            // pending tiles are flushed first so that no tile output is live
-            // across the out-of-line call)
+            // (rare: a big tile whose output exceeds a slot -- or, with
+            // QH_BIG_TILES 0, every big tile -- coded out of line after the
+            // pending tiles are flushed, so that no tile output is live across
+            // the call)
 #pragma unroll
             for (int i = 0; i < D; ++i)
                 if (pend[i].valid)
@@ -586,10 +647,11 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
                     l.poll(c);
                     flush_at(i, l, ~0u);
                 }
+            prof_stamp(c, kProfIters - 1, 0);    // (profiling) big tile
             pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
-                          status, n, LookBackBase{c, t});
+                          status, n);
+            prof_stamp(c, kProfIters - 1, 3);
         }
-#endif
         wave_sync();
         prof_stamp(c, it, 6);
 

@@ -68,6 +68,21 @@ def main():
                   " | base wait p50 %.0f max %.0f | output pass p50 %.0f max %.0f"
                   % (okb.sum(), np.median(a1), a1.max(), np.median(a2), a2.max(),
                      np.median(a3), a3.max()))
+        if tag == "decode":
+            q = p[:, 15, :]
+            okc = (q[:, 4] != 0) & (q[:, 8] != 0)
+            if okc.any():
+                A = q[okc, 5] - q[okc, 4]
+                B = q[okc, 6] - q[okc, 5]
+                Cn = q[okc, 7] - q[okc, 6]
+                Wt = q[okc, 8] - q[okc, 7]
+                rd = q[okc, 9]
+                print("  coop (last per wave, %d): A p50 %.0f p90 %.0f | B p50 %.0f"
+                      " p90 %.0f (rounds p50 %.0f max %d) | count p50 %.0f | W p50 %.0f"
+                      " p90 %.0f" % (okc.sum(), np.median(A), np.percentile(A, 90),
+                                     np.median(B), np.percentile(B, 90),
+                                     np.median(rd), rd.max(), np.median(Cn),
+                                     np.median(Wt), np.percentile(Wt, 90)))
         top = np.argsort(-codec)[:12]
         print("  slowest codecs: cycles | span maxhl ncoop nlong")
         for k in top:
