@@ -36,7 +36,7 @@ namespace qhuff {
 
 // Keep: the per-string entry points' kernel (DecPolicyT); a template
 // parameter, so the batch kernel's code and registers are untouched
-template <bool Keep>
+template <bool Keep, bool Full>
 __global__ __launch_bounds__(64 * kWaves) void
 qhuff_decode_kernel(DecArgs a)
 {
@@ -69,7 +69,7 @@ qhuff_decode_kernel(DecArgs a)
     // __syncthreads() would drain them)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     prof_realtime(a.c, kProfIters - 1, 11);      // (profiling) after it
-    DecPolicyT<DecSmem, Keep> pol{a.in, sm,
+    DecPolicyT<DecSmem, Keep, Full> pol{a.in, sm,
                                   &sm->w[__builtin_amdgcn_readfirstlane(tid >> 6)], 0};
 #ifdef QHUFF_PROFILE
     pol.pc = &a.c;
@@ -97,16 +97,22 @@ qhuff_decode_kernel(DecArgs a)
 
 hipError_t
 launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st, hipEvent_t ev0,
-              hipEvent_t ev1, bool keep)
+              hipEvent_t ev1, bool keep, bool full)
 {
     if (keep)
-        hipLaunchKernelGGL(qhuff_decode_kernel<true>, dim3(grid),
+        hipLaunchKernelGGL((qhuff_decode_kernel<true, false>), dim3(grid),
+                           dim3(64 * kWaves), 0, st, a);
+    else if (full && ev0)
+        hipExtLaunchKernelGGL((qhuff_decode_kernel<false, true>), dim3(grid),
+                              dim3(64 * kWaves), 0, st, ev0, ev1, 0, a);
+    else if (full)
+        hipLaunchKernelGGL((qhuff_decode_kernel<false, true>), dim3(grid),
                            dim3(64 * kWaves), 0, st, a);
     else if (ev0)
-        hipExtLaunchKernelGGL(qhuff_decode_kernel<false>, dim3(grid),
+        hipExtLaunchKernelGGL((qhuff_decode_kernel<false, false>), dim3(grid),
                               dim3(64 * kWaves), 0, st, ev0, ev1, 0, a);
     else
-        hipLaunchKernelGGL(qhuff_decode_kernel<false>, dim3(grid),
+        hipLaunchKernelGGL((qhuff_decode_kernel<false, false>), dim3(grid),
                            dim3(64 * kWaves), 0, st, a);
     return hipGetLastError();
 }
@@ -115,7 +121,7 @@ hipError_t
 decode_occupancy(int *blocks_per_cu)
 {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        blocks_per_cu, reinterpret_cast<const void *>(qhuff_decode_kernel<false>),
+        blocks_per_cu, reinterpret_cast<const void *>(qhuff_decode_kernel<false, true>),
         64 * kWaves, 0);
 }
 
@@ -135,7 +141,7 @@ size_t
 decode_lds_bytes()
 {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(qhuff_decode_kernel<false>))
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(qhuff_decode_kernel<false, true>))
             != hipSuccess)
         return 0;
     return fa.sharedSizeBytes;

@@ -486,6 +486,10 @@ write_bytes(QH_LDS uint8_t *d, uint32_t v, uint32_t nb)
 #ifndef QH_COOP_MIN
 #define QH_COOP_MIN 128
 #endif
+#ifndef QH_DEC_COOP                          // 0: every string by its lane
+                                             // (full kernel too)
+#define QH_DEC_COOP 1
+#endif
 constexpr uint32_t kCoopMin = QH_COOP_MIN;      // Huffman bytes
 #ifndef QH_SEG_MIN
 #define QH_SEG_MIN 128
@@ -539,18 +543,31 @@ seg_walk(const QH_LDS uint32_t *src, uint32_t &pos, uint32_t lim,
         const uint32_t w = bm[live ? r >> 5 : 0u];
         return live & (((w >> (r & 31)) & 1u) != 0);
     };
+    // (Mark) the bitmap word being filled, in a register: a lane's marks
+    // lie in its own segment, whose words it owns whole (segments are
+    // multiples of 32 bits from b0), and come in increasing order, so each
+    // word is stored whole with plain stores -- no atomics, no lane branch
+    uint32_t mi = (pos - b0) >> 5, mw = 0;
+    auto mark = [&](uint32_t r, bool on) {
+        const uint32_t wi = r >> 5;
+        const bool nw = on & (wi != mi);
+        mw = nw ? 0u : mw;
+        mi = nw ? wi : mi;
+        mw |= on ? 1u << (r & 31) : 0u;
+    };
     auto hook = [&](uint32_t e, uint32_t nb, uint32_t l0) {
         if constexpr (Mode == kWalkMark)
         {
-            const uint32_t r0 = pos - b0, r1 = r0 + l0;
+            const uint32_t r0 = pos - b0;
+            mark(r0, nb >= 1);
+            // the first symbol's word is complete if the second moves on
+            const uint32_t r1 = r0 + l0;
+            const bool two = nb == 2;
+            if (two & ((r1 >> 5) != mi))
+                bm[mi] = mw;
+            mark(r1, two);
             if (nb >= 1)
-                __hip_atomic_fetch_or(&bm[r0 >> 5], 1u << (r0 & 31),
-                                      __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (nb == 2)
-                __hip_atomic_fetch_or(&bm[r1 >> 5], 1u << (r1 & 31),
-                                      __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                bm[mi] = mw;
         }
         else if constexpr (Mode == kWalkEmit)
         {
@@ -965,10 +982,16 @@ dec_big_sizes(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
 // entry points use to replay where the reference stops on an invalid
 // string, qhuff_shim.cpp): a rejected string keeps, as its output, the bytes
 // decoded before the error; its status is QHUFF_DEC_ERROR all the same.
-template <class SM, bool Keep = false>
+template <class SM, bool Keep = false, bool Full = true>
 struct DecPolicyT
 {
     static constexpr bool kStatus = true;
+    // Full: the kernel for batches with big tiles (output slots) and long
+    // strings (coop_phase after the codec); the lean one codes those tiles
+    // out of line and its strings by their lanes, and its hot loop keeps its
+    // registers (qhuff_host.cpp picks the kernel per launch)
+    static constexpr bool kBig = Full;
+    static constexpr bool kCoop = Full && QH_DEC_COOP;
     static constexpr int kInCap = kDecInCap;
     static constexpr int kDepth = QH_DEPTH;       // pending tiles
     static constexpr int kOutCap = kDecStageCap;
@@ -980,6 +1003,8 @@ struct DecPolicyT
     QH_LDS DecWave *wv;
     uint32_t slot0;                  // this lane's arena slot (current tile)
     uint64_t coop = 0;               // strings decoded by the whole wave
+    bool hint = false;               // the tile has a string for coop_phase
+    __device__ __forceinline__ bool rare_hint() const { return hint; }
 #ifdef QHUFF_PROFILE
     const Coord *pc = nullptr;       // (profiling) stamps of coop_decode
 #endif
@@ -1024,7 +1049,8 @@ struct DecPolicyT
             2 * kDecTS + (uint32_t) ((8ull * (read_lane(to.o1, cnt - 1) - A)) / 5)
             + 2;
         // candidates in lane order while their bitmaps fit (at most 48)
-        const bool cand = !fixed && valid && hl > kCoopMin;
+        hint = !fixed && __builtin_amdgcn_ballot_w64(valid & (hl > kCoopMin));
+        const bool cand = kCoop && !fixed && valid && hl > kCoopMin;
         const uint32_t bmb = cand ? 4 * (hl / 4 + 2) : 0u;
         const uint32_t bm0 = (slots_end + 3) & ~3u;
         const uint32_t bmi = all_lanes(wave_incl_scan(bmb));
@@ -1034,59 +1060,80 @@ struct DecPolicyT
             coop = 0;
         const bool mine = (coop >> lane) & 1;
         int r = 0;
-#ifdef QH_COOP_DEBUG
-        bool dbg_fb = false;
-#endif
         if (valid)
         {
             ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
             r = decode_string_lds(wv->in, 8 * rs, mine ? 8 * rs : 8 * re,
                                   sm->win, sm->sorted, em);
         }
-        if (coop)
-        {
-            const int rc = coop_decode(
-                wv->in, coop, rs, re, slot0, wv->arena,
-                (QH_LDS uint32_t *) (wv->arena + bm0),
-                wv->arena + kArenaBytes - kCoopDummy, sm->win, sm->sorted
-#ifdef QHUFF_PROFILE
-                , pc
-#endif
-                );
-            r = mine ? rc : r;
-            const uint64_t fail = __builtin_amdgcn_ballot_w64(mine & (rc < 0));
-#ifdef QH_COOP_DEBUG
-            if (fail)
-            {
-                const bool f = (fail >> lane) & 1;
-                r = f ? 32 : r;
-                dbg_fb = f;
-                coop &= ~fail;
-            }
-            if (false)
-#else
-            if (fail)
-#endif
-            {
-                // (rare) an invalid string: its own lane decodes it again
-                // (the other lanes' two stores go to their sink bytes)
-                coop &= ~fail;
-                const bool f = (fail >> lane) & 1;
-                QH_LDS uint8_t *d0 = f ? wv->arena + slot0
-                                       : wv->arena + kArenaBytes - kCoopDummy
-                                             + 2 * lane;
-                ArenaEmit em{d0, d0, 0};
-                const int r2 = decode_string_lds(wv->in, 8 * rs,
-                                                 f ? 8 * re : 8 * rs, sm->win,
-                                                 sm->sorted, em);
-                r = f ? r2 : r;
-            }
-        }
         *sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
         *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+    }
+    // The strings flagged in `coop` by the codec, with the whole wave
+    // (coop_decode), into their sizes and statuses.  A separate step: the
+    // tile loop first moves its pending tiles' outputs out of registers
+    // (qhuff_pipeline.h), so this code runs beside few live values.
+    __device__ __forceinline__ void coop_phase(const Offs &to, uint32_t lo,
+                                               uint32_t cnt, const Span &sp,
+                                               uint32_t *sz, uint32_t *st)
+    {
+        const uint32_t lane = lane_id();
+        const uint32_t A = read_lane(to.o0, lo);
+        const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
+        const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
+        const uint32_t slots_end =
+            2 * kDecTS + (uint32_t) ((8ull * (read_lane(to.o1, cnt - 1) - A)) / 5)
+            + 2;
+        const uint32_t bm0 = (slots_end + 3) & ~3u;
+        const bool mine = (coop >> lane) & 1;
 #ifdef QH_COOP_DEBUG
-        *st = dbg_fb ? 7u : *st;
+        bool dbg_fb = false;
 #endif
+        int r = 0;
+        const int rc = coop_decode(
+            wv->in, coop, rs, re, slot0, wv->arena,
+            (QH_LDS uint32_t *) (wv->arena + bm0),
+            wv->arena + kArenaBytes - kCoopDummy, sm->win, sm->sorted
+#ifdef QHUFF_PROFILE
+            , pc
+#endif
+            );
+        r = rc;
+        const uint64_t fail = __builtin_amdgcn_ballot_w64(mine & (rc < 0));
+#ifdef QH_COOP_DEBUG
+        if (fail)
+        {
+            const bool f = (fail >> lane) & 1;
+            r = f ? 32 : r;
+            dbg_fb = f;
+            coop &= ~fail;
+        }
+        if (false)
+#else
+        if (fail)
+#endif
+        {
+            // (rare) an invalid string: its own lane decodes it again
+            // (the other lanes' two stores go to their sink bytes)
+            coop &= ~fail;
+            const bool f = (fail >> lane) & 1;
+            QH_LDS uint8_t *d0 = f ? wv->arena + slot0
+                                   : wv->arena + kArenaBytes - kCoopDummy
+                                         + 2 * lane;
+            ArenaEmit em{d0, d0, 0};
+            const int r2 = decode_string_lds(wv->in, 8 * rs,
+                                             f ? 8 * re : 8 * rs, sm->win,
+                                             sm->sorted, em);
+            r = f ? r2 : r;
+        }
+        if (mine)
+        {
+            *sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
+            *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+#ifdef QH_COOP_DEBUG
+            *st = dbg_fb ? 7u : *st;
+#endif
+        }
     }
     // arena -> the (dead) input stage, compacted (the cooperative strings
     // by the whole wave, after the rest)
@@ -1163,7 +1210,7 @@ dec_big_sizes(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
               uint32_t cnt, TileOffs to, Span sp, uint32_t &sz, uint32_t &st,
               uint32_t slot0, uint8_t *dst)
 {
-    using P = DecPolicyT<SM, Keep>;
+    using P = DecPolicyT<SM, Keep, true>;
     P pol{in, sm, wv, 0};
     const uint32_t lane = lane_id();
     uint32_t run = 0;                        // output bytes so far (uniform)
@@ -1243,6 +1290,8 @@ dec_big_sizes(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
         stage_chunks<true>(su, (QH_LDS u32x4 *) wv->in);
         uint32_t s1, t1;
         pol.codec_range(to, i0, i0 + k, su, &s1, &t1);
+        if (pol.coop)
+            pol.coop_phase(to, i0, i0 + k, su, &s1, &t1);
         wave_sync();
         put(i0, i0 + k, s1, t1, pol.slot0);
         if ((lane >= i0) & (lane < i0 + k))

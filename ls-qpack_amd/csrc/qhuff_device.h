@@ -97,6 +97,9 @@ struct Coord
                                             // the grid covers; qhuff_pipeline.h)
     uint8_t *big;                           // big-tile output slots:
                                             // kBigSlots per wave of the grid
+    uint32_t *rare;                         // host-mapped word: set when the
+                                            // launch met tiles the full
+                                            // kernel is for (qhuff_host.cpp)
 };
 
 // A big tile's output (qhuff_pipeline.h) waits in one of its wave's

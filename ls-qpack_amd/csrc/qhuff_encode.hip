@@ -42,8 +42,7 @@
 
 namespace qhuff {
 
-using EncPolicy = EncPolicyT<EncSmem>;
-
+template <bool Full>
 __global__ __launch_bounds__(64 * kWaves) void
 qhuff_encode_kernel(EncArgs a)
 {
@@ -59,7 +58,7 @@ qhuff_encode_kernel(EncArgs a)
     claim_block_store(a.c, cb, &sm->tk, QH_ENC_PER);
     clear_next_launch(a.c);
     __syncthreads();                 // the only workgroup barrier
-    EncPolicy pol;
+    EncPolicyT<EncSmem, Full> pol;
     pol.in = a.in;
     pol.mode = a.mode;
     pol.sm = sm;
@@ -73,14 +72,20 @@ qhuff_encode_kernel(EncArgs a)
 
 hipError_t
 launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st, hipEvent_t ev0,
-              hipEvent_t ev1)
+              hipEvent_t ev1, bool full)
 {
-    if (ev0)
-        hipExtLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(64 * kWaves), 0, st,
-                              ev0, ev1, 0, a);
+    if (full && ev0)
+        hipExtLaunchKernelGGL(qhuff_encode_kernel<true>, dim3(grid),
+                              dim3(64 * kWaves), 0, st, ev0, ev1, 0, a);
+    else if (full)
+        hipLaunchKernelGGL(qhuff_encode_kernel<true>, dim3(grid),
+                           dim3(64 * kWaves), 0, st, a);
+    else if (ev0)
+        hipExtLaunchKernelGGL(qhuff_encode_kernel<false>, dim3(grid),
+                              dim3(64 * kWaves), 0, st, ev0, ev1, 0, a);
     else
-        hipLaunchKernelGGL(qhuff_encode_kernel, dim3(grid), dim3(64 * kWaves),
-                           0, st, a);
+        hipLaunchKernelGGL(qhuff_encode_kernel<false>, dim3(grid),
+                           dim3(64 * kWaves), 0, st, a);
     return hipGetLastError();
 }
 
@@ -88,7 +93,7 @@ hipError_t
 encode_occupancy(int *blocks_per_cu)
 {
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        blocks_per_cu, reinterpret_cast<const void *>(qhuff_encode_kernel),
+        blocks_per_cu, reinterpret_cast<const void *>(qhuff_encode_kernel<true>),
         64 * kWaves, 0);
 }
 
@@ -102,7 +107,7 @@ size_t
 encode_lds_bytes()
 {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(qhuff_encode_kernel))
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(qhuff_encode_kernel<true>))
             != hipSuccess)
         return 0;
     return fa.sharedSizeBytes;

@@ -25,7 +25,7 @@
 // table, several to a bank).  32 KB of LDS, which the batch kernel has
 // free; the service kernel keeps one copy.
 #ifndef QH_MT_REP
-#define QH_MT_REP 1
+#define QH_MT_REP 0
 #endif
 
 namespace qhuff {
@@ -665,6 +665,9 @@ copy_dense_mid(const QH_LDS uint32_t *dense, uint32_t s, uint32_t nb,
 #ifndef QH_ENC_COOP_BITS
 #define QH_ENC_COOP_BITS 1024
 #endif
+#ifndef QH_ENC_COOP                          // 0: every payload by its lane
+#define QH_ENC_COOP 1
+#endif
 constexpr uint32_t kEncCoopBits = QH_ENC_COOP_BITS;
 
 // one string from the dense stream: framing, payload bits [s, s + bits),
@@ -752,10 +755,16 @@ enc_big_sizes(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
 
 // the encode side of the wave pipeline (qhuff_pipeline.h, qhuff_service.hip);
 // SM: the workgroup's LDS (enc, mt, len)
-template <class SM>
+template <class SM, bool Full = true>
 struct EncPolicyT
 {
     static constexpr bool kStatus = false;
+    // Full: big tiles through output slots, long payloads copied by the
+    // wave (see DecPolicyT)
+    static constexpr bool kBig = Full;
+    static constexpr bool kCoop = false;          // (no coop_phase)
+    static constexpr uint64_t coop = 0;
+    __device__ __forceinline__ bool rare_hint() const { return false; }
     static constexpr int kInCap = kEncInCap;
     static constexpr int kDepth = QH_ENC_DEPTH;       // pending tiles
     static constexpr int kOutCap = kEncOutCap;
@@ -797,6 +806,11 @@ struct EncPolicyT
                                           uint32_t *st)
     {
         codec_range(to, 0, cnt, sp, sz, st);
+    }
+    __device__ __forceinline__ void coop_phase(const TileOffs &, uint32_t,
+                                               uint32_t, const Span &,
+                                               uint32_t *, uint32_t *)
+    {
     }
     // the strings of lanes [lo, cnt) (sp: their span, prepared)
     __device__ __forceinline__ void codec_range(const TileOffs &to, uint32_t lo,
@@ -843,7 +857,8 @@ struct EncPolicyT
         if (dense)
         {
             // long payloads: their middle words by the whole wave, after
-            const bool lc = (sz != 0) & z.huff & (bits > kEncCoopBits);
+            const bool lc = Full && QH_ENC_COOP && (sz != 0) & z.huff
+                          & (bits > kEncCoopBits);
             const uint64_t lm = __builtin_amdgcn_ballot_w64(lc);
             uint32_t p0 = 0;
             if (sz)
@@ -926,7 +941,7 @@ enc_big_sizes(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
               QH_LDS EncWave *wv, uint32_t cnt, TileOffs to, Span sp,
               uint32_t &sz, uint8_t *dst)
 {
-    using P = EncPolicyT<SM>;
+    using P = EncPolicyT<SM, true>;
     P pol{in, mode, sm, wv};
     const uint32_t lane = lane_id();
     const bool valid = lane < cnt;

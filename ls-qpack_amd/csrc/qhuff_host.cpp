@@ -154,6 +154,15 @@ struct qhuff_ctx
     uint64_t cap_tiles, cap_super;
     uint8_t *big;                        // device: big-tile output slots
                                          // (Coord::big), kBigSlots per wave
+    // kernel variant per kind (0 encode, 1 decode): the lean kernel by
+    // default; the full one (big-tile slots, cooperative long strings) once
+    // a launch reports such tiles, until kCalm launches in a row have none
+    uint32_t *rare_host;                 // pinned, device-mapped: [kind]
+    uint32_t *rare_dev;
+    bool full[2];
+    uint32_t calm[2];
+    int kernels;                         // QHUFF_KERNELS: 0 auto, 1 lean,
+                                         // 2 full
     unsigned long long *prof;            // QHUFF_PROFILE builds: stamp buffer
     size_t prof_words;
     uint32_t epoch;
@@ -291,6 +300,16 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         e = hipMalloc((void **) &c->big, waves * kBigSlots * kBigSlotBytes);
     }
     if (e == hipSuccess)
+        e = hipHostMalloc((void **) &c->rare_host, 4 * sizeof(uint32_t),
+                          hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess)
+    {
+        memset(c->rare_host, 0, 4 * sizeof(uint32_t));
+        e = hipHostGetDevicePointer((void **) &c->rare_dev, c->rare_host, 0);
+        const char *kv = getenv("QHUFF_KERNELS");
+        c->kernels = !kv ? 0 : !strcmp(kv, "lean") ? 1 : !strcmp(kv, "full") ? 2 : 0;
+    }
+    if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming);
@@ -354,6 +373,8 @@ qhuff_close(qhuff_ctx *c)
         (void) hipFree(c->flags);
     if (c->big)
         (void) hipFree(c->big);
+    if (c->rare_host)
+        (void) hipHostFree(c->rare_host);
     if (c->err)
         (void) hipFree(c->err);
     if (c->d_stage)
@@ -541,6 +562,7 @@ coord(qhuff_ctx *c, uint64_t tiles)
     k.n_tiles = (uint32_t) tiles;
     k.spread = 0;
     k.big = c->big;
+    k.rare = nullptr;
     return k;
 }
 
@@ -640,6 +662,32 @@ grid_for(const qhuff_ctx *c, uint64_t tiles, uint64_t waves_per_block,
     return (uint32_t) (need < cap ? need : cap);
 }
 
+// The kernel variant of the next launch of `kind` (0 encode, 1 decode),
+// and where it reports rare tiles.  A launch that met big tiles or long
+// strings sets rare_host[kind] (qhuff_pipeline.h); the flag is read here,
+// without waiting for any launch, so the switch to the full kernel lands a
+// launch or two after the data changes.  (The lean kernel codes those tiles
+// correctly but slowly; the full one carries their code beside the tile
+// loop, which costs the loop ~5 % on batches that never need it.)
+static constexpr uint32_t kCalm = 8;
+static bool
+pick_full(qhuff_ctx *c, int kind, Coord *k)
+{
+    k->rare = c->rare_dev + kind;
+    if (c->kernels)
+        return c->kernels == 2;
+    volatile uint32_t *r = c->rare_host + kind;
+    if (*r)
+    {
+        *r = 0;
+        c->full[kind] = true;
+        c->calm[kind] = 0;
+    }
+    else if (c->full[kind] && ++c->calm[kind] >= kCalm)
+        c->full[kind] = false;
+    return c->full[kind];
+}
+
 extern "C" int
 qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
                    uint32_t n, unsigned mode, uint8_t *out, uint32_t *out_off,
@@ -673,7 +721,8 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     const uint32_t grid = grid_for(c, tiles, wpb, c->enc_grid, &a.c.spread);
     hipEvent_t e0, e1;
     timing_slot(c, QHUFF_KIND_ENCODE, &e0, &e1);
-    HIPCHK(c, launch_encode(a, grid, st, e0, e1));
+    const bool full = pick_full(c, 0, &a.c);
+    HIPCHK(c, launch_encode(a, grid, st, e0, e1, full));
     return finish_launch(c, st);
 }
 
@@ -711,7 +760,8 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     const uint32_t grid = grid_for(c, tiles, wpb, c->dec_grid, &a.c.spread);
     hipEvent_t e0, e1;
     timing_slot(c, QHUFF_KIND_DECODE, &e0, &e1);
-    HIPCHK(c, launch_decode(a, grid, st, e0, e1, c->keep_rejected));
+    const bool full = pick_full(c, 1, &a.c);
+    HIPCHK(c, launch_decode(a, grid, st, e0, e1, c->keep_rejected, full));
     return finish_launch(c, st);
 }
 

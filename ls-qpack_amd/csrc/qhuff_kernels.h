@@ -143,13 +143,16 @@ glb(T *p)
 
 // ev0 / ev1 non-null: the launch records its own start / stop time in them
 // (hipExtLaunchKernelGGL: the dispatch's timestamps, no extra queue packets)
+// full: the kernel variant with big-tile slots and cooperative long strings
+// (qhuff_pipeline.h); the lean one is the default (qhuff_host.cpp)
 hipError_t launch_encode(const EncArgs &a, uint32_t grid, hipStream_t st,
-                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
+                         bool full = false);
 // keep: the kernel that keeps a rejected string's bytes decoded before its
 // error (qhuff_shim.cpp)
 hipError_t launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st,
                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
-                         bool keep = false);
+                         bool keep = false, bool full = false);
 hipError_t launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st,
                        hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t hash_occupancy(int *blocks_per_cu);

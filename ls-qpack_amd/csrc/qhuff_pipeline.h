@@ -39,13 +39,6 @@
 
 #include "qhuff_kernels.h"
 
-// Big tiles (input or output past the stages) sized in staged units and
-// their output written to a per-wave slot, then pending like any other tile
-// (qhuff_*_impl.h *_big_sizes); 0: the round-3 path only, an out-of-line
-// per-lane walk over global memory after the pending tiles are flushed.
-#ifndef QH_BIG_TILES
-#define QH_BIG_TILES 1
-#endif
 
 namespace qhuff {
 
@@ -469,6 +462,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         pend[i].big = 0;
     }
     uint32_t big_next = 0;                   // big-tile slots used (ring)
+    bool rare = false;                       // met a big or cooperative tile
     uint32_t it = 0;
     for (;; ++it)
     {
@@ -521,27 +515,10 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         const uint32_t cnt = cnt_of(t);
         uint32_t sz = 0, st = 0;
         bool fast = sp_cur.staged;
-        if (fast)
-        {
-            pol.prepare(sp_cur);
-            pol.codec(o_cur, cnt, sp_cur, &sz, &st);
-        }
-        uint32_t incl = wave_incl_scan(sz);
-        uint32_t excl = incl - sz;
-        uint32_t total = read_lane(incl, 63);
-        fast = fast && total + 64 <= (uint32_t) P::kOutCap;
-#if QH_BIG_TILES
-        // A big tile (input or output past the stages): its sizes, in
-        // staged units, and its output into one of the wave's big-tile slots
-        // (P::big_sizes).  When it fits, it is pending like any other tile
-        // from here on -- its output copied from the slot when its look-back
-        // resolves -- and the wave goes straight on to its next tile.
-        uint32_t bigslot = 0;                // (wave-uniform) 1 + the slot
-        if (!fast)
-        {
-            // the pending tiles' outputs move to slots first, so that their
-            // registers are free for the big tile's codec (the slots hold
-            // every tile in flight: kDepth pending + this one)
+        // the pending tiles' outputs to slots (their registers are free
+        // for the big-tile or cooperative code that follows)
+        auto park = [&]() {
+            if constexpr (P::kBig)
 #pragma unroll
             for (int i = 0; i < D; ++i)
             {
@@ -554,22 +531,51 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
                 }
                 outs[i].clear();
             }
-            const uint32_t k = big_next % kBigSlots;
-            if (pol.big_sizes(cnt, o_cur, sp_cur, sz, st, big_slot(c, k)))
+        };
+        if (fast)
+        {
+            pol.prepare(sp_cur);
+            pol.codec(o_cur, cnt, sp_cur, &sz, &st);
+            if (P::kCoop && pol.coop)
             {
-                bigslot = k + 1;
-                ++big_next;
+                park();
+                pol.coop_phase(o_cur, 0, cnt, sp_cur, &sz, &st);
             }
-            incl = wave_incl_scan(sz);
-            excl = incl - sz;
-            total = read_lane(incl, 63);
-            // the next tile's input again: its chunk registers were free
-            // through the big tile's codec
-            ch.load(sp_nxt);
+            rare |= pol.rare_hint();
         }
-#else
-        constexpr uint32_t bigslot = 0;
-#endif
+        uint32_t incl = wave_incl_scan(sz);
+        uint32_t excl = incl - sz;
+        uint32_t total = read_lane(incl, 63);
+        fast = fast && total + 64 <= (uint32_t) P::kOutCap;
+        uint32_t bigslot = 0;                // (wave-uniform) 1 + the slot
+        if constexpr (P::kBig)
+        {
+            // A big tile (input or output past the stages): its sizes, in
+            // staged units, and its output into one of the wave's big-tile slots
+            // (P::big_sizes).  When it fits, it is pending like any other tile
+            // from here on -- its output copied from the slot when its look-back
+            // resolves -- and the wave goes straight on to its next tile.
+            if (!fast)
+            {
+                rare = true;
+                // the pending tiles' outputs move to slots first, so that their
+                // registers are free for the big tile's codec (the slots hold
+                // every tile in flight: kDepth pending + this one)
+                park();
+                const uint32_t k = big_next % kBigSlots;
+                if (pol.big_sizes(cnt, o_cur, sp_cur, sz, st, big_slot(c, k)))
+                {
+                    bigslot = k + 1;
+                    ++big_next;
+                }
+                incl = wave_incl_scan(sz);
+                excl = incl - sz;
+                total = read_lane(incl, 63);
+                // the next tile's input again: its chunk registers were free
+                // through the big tile's codec
+                ch.load(sp_nxt);
+            }
+        }
         prof_stamp(c, it, 3);
 
         Pending cur;
@@ -635,6 +641,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
             outs[D - 1].clear();             // (its output is in its slot)
         else
         {
+            rare = true;
             // (rare: a big tile whose output exceeds a slot -- or, with
             // QH_BIG_TILES 0, every big tile -- coded out of line after the
             // pending tiles are flushed, so that no tile output is live across
@@ -682,6 +689,11 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     // (The wave claimed until a claim landed past the end, so every ticket
     // of its group is taken, by running waves: see BlockTickets.  A spread
     // launch hands out a prefix of the tiles, one per wave.)
+    // the launch met tiles the full kernel is for: tell the host (one store
+    // per wave that did; qhuff_host.cpp picks the next launch's kernel)
+    if (rare && c.rare && lane_id() == 0)
+        __hip_atomic_store(c.rare, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace qhuff

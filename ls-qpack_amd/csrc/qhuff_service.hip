@@ -130,6 +130,8 @@ serve_tiles(P &pol, const uint8_t *in, const uint32_t *in_off, uint32_t n,
         {
             pol.prepare(sp);
             pol.codec(o, cnt, sp, &sz, &st);
+            if (P::kCoop && pol.coop)
+                pol.coop_phase(o, 0, cnt, sp, &sz, &st);
         }
         const uint32_t incl = wave_incl_scan(sz);
         const uint32_t excl = incl - sz;

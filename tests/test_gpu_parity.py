@@ -246,6 +246,41 @@ def test_multi_unit_tiles(codec, lo, hi):
     assert codec.device_error() == 0
 
 
+def test_big_tile_slots(codec):
+    """Tiles past the stages whose output fits a big-tile slot (12 KB,
+    qhuff_pipeline.h): one string of 3.2-5 KB among short ones (input past
+    the stage: the string walked in global memory into the slot), runs of
+    ~1 KB strings (several staged units), and tiles just over the stage;
+    mixed with ordinary tiles so big tiles sit among pending ones."""
+    rng = random.Random(77)
+    strs = []
+    for t in range(60):
+        k = t % 3
+        if k == 0:
+            tile = (rand_strings(rng, 63, ALPHAS["token"], 0, 20)
+                    + rand_strings(rng, 1, ALPHAS["token"], 3200, 5000))
+        elif k == 1:
+            tile = rand_strings(rng, 8, ALPHAS["all"], 600, 1100) \
+                + rand_strings(rng, 56, ALPHAS["token"], 0, 30)
+        else:
+            tile = rand_strings(rng, 64, ALPHAS["token"], 40, 70)
+        rng.shuffle(tile)
+        strs += tile
+        strs += rand_strings(rng, 64 * 3, ALPHAS["token"], 8, 40)
+    data, off = pack(strs)
+    for mode in (0, 5, 7):
+        check_encode(codec, data, off, mode)
+    h, ho = O.encode_batch(data, off, 0)
+    out, oo, st = check_decode(codec, h, ho)
+    assert not st.any() and np.array_equal(out, data)
+    # and invalid strings inside big tiles (statuses and sizes as the oracle)
+    h2 = h.copy()
+    for i in range(5, len(ho) - 1, 41):
+        if ho[i + 1] > ho[i]:
+            h2[ho[i + 1] - 1] ^= 0x33
+    check_decode(codec, h2, ho)
+
+
 def test_edge_batches(codec):
     # n = 0
     for mode in (0, 7):
@@ -334,6 +369,32 @@ def test_decode_cooperative_invalid(codec):
                             corrupt)
     out, oo, st = check_decode(codec, data, off)
     assert st.sum() > 20 and (st == 0).sum() > 1000
+
+
+@pytest.mark.parametrize("kernels", ["lean", "full", "auto"])
+def test_kernel_variants(kernels):
+    """Each kernel of a kind is exact on its own (qhuff_host.cpp pick_full):
+    the lean one, which codes big tiles and long strings on the round-3 path,
+    the full one (big-tile slots, cooperative long strings), and the switch
+    between them -- auto starts lean, and its later launches of the same
+    batches run full once the rare flag is set; each case is run twice."""
+    import qhuff
+    old = os.environ.get("QHUFF_KERNELS")
+    os.environ["QHUFF_KERNELS"] = kernels
+    try:
+        c = qhuff.Codec(0)
+    finally:
+        if old is None:
+            del os.environ["QHUFF_KERNELS"]
+        else:
+            os.environ["QHUFF_KERNELS"] = old
+    try:
+        for _ in range(2):
+            test_big_tile_slots(c)
+            test_decode_cooperative_long_strings(c, "token")
+            test_decode_cooperative_invalid(c)
+    finally:
+        c.close()
 
 
 def _launch_shape_check(c, n, seed):
