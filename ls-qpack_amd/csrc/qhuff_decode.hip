@@ -27,9 +27,9 @@
 
 #include <hip/hip_ext.h>
 
-// tickets claimed per wave in the prologue, at most (tile_pipeline)
+// tickets claimed per wave in the prologue, at most (see qhuff_encode.hip)
 #ifndef QH_DEC_PER
-#define QH_DEC_PER 3
+#define QH_DEC_PER 2
 #endif
 
 namespace qhuff {

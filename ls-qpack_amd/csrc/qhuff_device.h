@@ -298,14 +298,15 @@ struct Tickets
     {
         return &c.tick[((c.epoch & 1) * kTickGroups + q) * kTickStride];
     }
-    __device__ __forceinline__ uint32_t claim(const Coord &c) const
+    // claims `m` consecutive tickets of the group; returns the first
+    __device__ __forceinline__ uint32_t claim(const Coord &c, uint32_t m = 1) const
     {
         uint32_t k = 0, q = g;
         // (the opaque copy keeps the counter address from being hoisted
         // out of the tile loop: held there it was a spilled register pair)
         asm volatile("" : "+v"(q));
         if (lane_id() == 0)
-            k = __hip_atomic_fetch_add(counter(c, q), 1u, __ATOMIC_RELAXED,
+            k = __hip_atomic_fetch_add(counter(c, q), m, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         return k;
     }

@@ -25,19 +25,22 @@
 //      staged input;
 //   4. look-back for the tile's global output base, 16-byte stores
 //      (qhuff_pipeline.h).
-// A tile holding a code longer than 15 bits (control and high bytes) or
-// whose dense stream overflows is sized and packed string per lane from the
-// staged input instead; tiles that do not fit the stages take the slow path
-// (global reads / per-lane global writes).
+// A tile whose dense stream overflows its buffer is sized and packed string
+// per lane from the staged input instead (codes of any length go into the
+// dense stream); tiles that do not fit the stages are big tiles
+// (qhuff_pipeline.h).
 #include "qhuff_encode_impl.h"
 
 #include <hip/hip_ext.h>
 
-// tickets claimed per wave in the prologue, at most (tile_pipeline); 3
-// since the encode runs three pending tiles (0.971 of 2 + the late third
-// ticket, four pairs: profiles/r03_ep3)
+// tickets claimed per wave in the prologue, at most (tile_pipeline).  2: the
+// third and fourth tickets are claimed by each wave at its first top, after
+// every workgroup's first claims (tile_pipeline `late`).  3 (round 3,
+// profiles/r03_ep3) put every workgroup's third tiles ahead of later
+// workgroups' first ones, and the first flush waited for the slowest of
+// them (profiles/r04_r; r04_s: first flush 10.4k -> 3.1k cycles).
 #ifndef QH_ENC_PER
-#define QH_ENC_PER 3
+#define QH_ENC_PER 2
 #endif
 
 namespace qhuff {

@@ -262,11 +262,10 @@ wait_vm_all()
 // share with one returning atomic (~3,000 waves claiming one by one would
 // queue on the counters).  A wave of group g that is the r-th of its group
 // in the workgroup gets tickets base + r, base + n_g + r and base + 2 n_g + r
-// (n_g waves of the workgroup in group g).  Three tickets per wave when the
-// tiles cover three per wave of the whole grid (the third replaces the
-// wave's own first claim, whose burst of ~3,000 returning adds the first
-// iteration would wait for), else two; a ticket not claimed here is
-// kClaimNow: the wave claims it itself once it runs, like every later one.
+// (n_g waves of the workgroup in group g).  Two tickets per wave (the
+// kernels' maxper; three when maxper allows it and the tiles cover three
+// per wave of the whole grid); a ticket not claimed here is kClaimNow: the
+// wave claims it itself once it runs, like every later one.
 // Every wave goes on claiming until a claim lands past the end, so no
 // ticket of any group is left to a workgroup that is not running -- a tile
 // fixed to whichever workgroup claimed it would need the whole grid
@@ -422,13 +421,16 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     // tile is always coded (tickets of a group are handed out in order, so
     // once tn is past the end every later claim is too)
     const uint32_t kNone = 0xffffffffu;
-    // late: the third ticket is claimed by the wave after the first tile's
-    // input loads, and the first iteration's top does not wait for it (a
-    // burst of ~3,000 returning adds on 8 counters takes microseconds); that
-    // iteration reads it after its codec and loads the third tile's offsets
-    // then (tickets claimed by the workgroup in the prologue instead would
-    // hand each workgroup a third tile ahead of other workgroups' first and
-    // second ones, whose look-backs then wait on third tiles: profiles/r03_u)
+    // late: the third and fourth tickets are claimed by the wave together,
+    // at the first iteration's top, and read after its codec (a burst of
+    // ~3,000 returning adds on 8 counters takes microseconds); that
+    // iteration loads the third tile's offsets then.  Tickets claimed by the
+    // workgroup in the prologue instead hand each workgroup a third tile
+    // ahead of other workgroups' first ones, whose first flush then waits on
+    // the slowest of those third tiles (profiles/r03_u, r04_r: look-back
+    // 3.7 us at the median).  (Claimed in the prologue, after the first
+    // loads, the claim was waited for at the loop's entry: the compiler's
+    // vmcnt(0) for its result's copy, r04_r.)
     const bool late = tn < nt && k1 != kClaimNow && k2 == kClaimNow;
     uint32_t kq = tn < nt ? (k2 == kClaimNow ? 0u : k2) : kNone;
     if (tn < nt && k2 == kClaimNow && !late)
@@ -437,9 +439,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     Span sp_cur = tile_span(in, o_cur.first(), o_cur.last(), P::kInCap);
     Chunks<P::kNch> ch;
     ch.load(sp_cur);
-    if (late)
-        kq = tk.claim(c);                    // the youngest operation
-    uint32_t kq4 = 0;                        // (late) the fourth ticket
+    uint32_t kq4 = 0;                        // (late) the third ticket
 
     // Tiles come from in-order tickets claimed two iterations ahead (one
     // claim per wave per iteration), so the order in which a wave claims
@@ -479,10 +479,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         // 65.6 / dec 68.7 vs 65.3 / 68.3 us, interleaved A/B, profiles/r02_g)
         // -- the waves then wait longer in their look-backs.
         const bool defer = late && it == 0;  // (wave-uniform)
-        if (defer)
-            __builtin_amdgcn_s_waitcnt(0x0f71);  // all but the late claim
-        else
-            wait_vm_all();
+        wait_vm_all();
         prof_stamp(c, it, 1);
         if (sp_cur.staged)
             pol.stage_in(ch, sp_cur, o_cur);
@@ -502,7 +499,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
             kq = tnn < nt ? tk.claim(c) : kNone;
         }
         else
-            kq4 = tk.claim(c);               // (past the end: never coded)
+            kq4 = tk.claim(c, 2);            // third and fourth tickets
         LookBack lbo;                        // the oldest pending tile's
         if (pend[0].valid)
         {
@@ -612,11 +609,11 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         prof_stamp(c, it, 4);
         if (defer)
         {
-            // the late third ticket has landed: its tile's offsets now
-            tnn = tn < nt ? tk.tile_of(kq) : kNone;
+            // the late tickets have landed: the third tile's offsets now
+            tnn = tk.tile_of(kq4);
             const uint32_t tz = clamp(tnn);
             o_nn.load(in_off, (uint64_t) tz * TS, cnt_of(tz));
-            kq = kq4;
+            kq = tnn < nt ? kq4 + 1 : kNone;
         }
         // t's add has returned with the polls: publish its super tile's
         // aggregate if that add completed it -- here, an emit after the add,
@@ -671,6 +668,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         sp_cur = sp_nxt;
     }
     wait_vm_all();
+    prof_stamp(c, kProfIters - 2, 6);        // (profiling) drain start
     // the drain: every pending tile's polls issued together, then each one
     // resolved and stored (one round trip for all of them, not one each:
     // the last waves' drain ends the kernel)
@@ -686,6 +684,11 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     for (int i = 0; i < D; ++i)
         if (pend[i].valid)
             flush_at(i, ld[i], ~0u);
+#ifdef QHUFF_PROFILE
+    wait_vm_all();
+    prof_stamp(c, kProfIters - 2, 7);        // (profiling) drain end
+    prof_realtime(c, kProfIters - 2, 8);
+#endif
     // (The wave claimed until a claim landed past the end, so every ticket
     // of its group is taken, by running waves: see BlockTickets.  A spread
     // launch hands out a prefix of the tiles, one per wave.)
