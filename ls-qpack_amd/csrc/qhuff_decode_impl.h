@@ -1219,7 +1219,7 @@ dec_big_sizes(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
     auto put = [&](uint32_t lo, uint32_t hi, uint32_t s, uint32_t t,
                    uint32_t slot) {
         const bool in_u = (lane >= lo) & (lane < hi);
-        const uint32_t ls = in_u & (Keep || t == QHUFF_DEC_OK) ? s : 0u;
+        const uint32_t ls = (in_u && (Keep || t == QHUFF_DEC_OK)) ? s : 0u;
         const uint32_t incl = all_lanes(wave_incl_scan(ls));
         const uint32_t ut = read_lane(incl, 63);
         fits = fits && run + ut <= kBigSlotBytes;

@@ -97,9 +97,12 @@ struct Coord
                                             // the grid covers; qhuff_pipeline.h)
     uint8_t *big;                           // big-tile output slots:
                                             // kBigSlots per wave of the grid
-    uint32_t *rare;                         // host-mapped word: set when the
-                                            // launch met tiles the full
-                                            // kernel is for (qhuff_host.cpp)
+    uint32_t *rare;                         // host-mapped words: [0] set
+                                            // when the launch met tiles the
+                                            // full kernel is for, [1] the
+                                            // epoch of the launch once it
+                                            // started (qhuff_host.cpp
+                                            // pick_full)
 };
 
 // A big tile's output (qhuff_pipeline.h) waits in one of its wave's

@@ -157,10 +157,12 @@ struct qhuff_ctx
     // kernel variant per kind (0 encode, 1 decode): the lean kernel by
     // default; the full one (big-tile slots, cooperative long strings) once
     // a launch reports such tiles, until kCalm launches in a row have none
-    uint32_t *rare_host;                 // pinned, device-mapped: [kind]
+    uint32_t *rare_host;                 // pinned, device-mapped: [2 kind],
+                                         // [2 kind + 1] (pick_full)
     uint32_t *rare_dev;
     bool full[2];
     uint32_t calm[2];
+    uint32_t seen[2];                    // rare_host[2 kind + 1] last read
     int kernels;                         // QHUFF_KERNELS: 0 auto, 1 lean,
                                          // 2 full
     unsigned long long *prof;            // QHUFF_PROFILE builds: stamp buffer
@@ -663,28 +665,41 @@ grid_for(const qhuff_ctx *c, uint64_t tiles, uint64_t waves_per_block,
 }
 
 // The kernel variant of the next launch of `kind` (0 encode, 1 decode),
-// and where it reports rare tiles.  A launch that met big tiles or long
-// strings sets rare_host[kind] (qhuff_pipeline.h); the flag is read here,
+// and where it reports.  Per kind two words of pinned, device-mapped host
+// memory: [0] set by a launch that met big tiles or long strings (at its
+// end), [1] the epoch of the last launch that started (block 0, at its
+// start: every earlier launch of the stream has ended).  Both are read here
 // without waiting for any launch, so the switch to the full kernel lands a
-// launch or two after the data changes.  (The lean kernel codes those tiles
-// correctly but slowly; the full one carries their code beside the tile
-// loop, which costs the loop ~5 % on batches that never need it.)
+// launch or two after the data changes, and the way back needs kCalm
+// launches seen to have run -- not issued: a burst of launches is issued
+// long before the first of them reports.  (The lean kernel codes those
+// tiles correctly but slowly; the full one carries their code beside the
+// tile loop, which costs the loop ~5 % on batches that never need it.)
 static constexpr uint32_t kCalm = 8;
 static bool
 pick_full(qhuff_ctx *c, int kind, Coord *k)
 {
-    k->rare = c->rare_dev + kind;
+    k->rare = c->rare_dev + 2 * kind;
     if (c->kernels)
         return c->kernels == 2;
-    volatile uint32_t *r = c->rare_host + kind;
-    if (*r)
+    volatile uint32_t *r = c->rare_host + 2 * kind;
+    if (r[0])
     {
-        *r = 0;
+        r[0] = 0;
         c->full[kind] = true;
         c->calm[kind] = 0;
+        c->seen[kind] = r[1];
     }
-    else if (c->full[kind] && ++c->calm[kind] >= kCalm)
-        c->full[kind] = false;
+    else if (c->full[kind])
+    {
+        const uint32_t s = r[1];
+        if (s != c->seen[kind])
+        {
+            c->seen[kind] = s;
+            if (++c->calm[kind] >= kCalm)
+                c->full[kind] = false;
+        }
+    }
     return c->full[kind];
 }
 

@@ -392,6 +392,11 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
 {
     const QH_GLB uint32_t *in_off = (const QH_GLB uint32_t *) in_off_p;
     const uint32_t nt = c.n_tiles;
+    // the launch has started (qhuff_host.cpp pick_full: every earlier launch
+    // of the stream has ended, and reported)
+    if (c.rare && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(c.rare + 1, c.epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     // this wave's first tile t0 and the tickets k1 < k2 of its next ones
     // (claimed for the whole block in the kernel prologue, or kClaimNow)
     uint32_t t = t0;
