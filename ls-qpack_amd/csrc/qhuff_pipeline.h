@@ -7,22 +7,22 @@
 // look-back waits on belongs to a running wave, whatever the residency.
 // Per iteration, for tile t:
 //
-//   top    one wait for what the last iteration issued: t's input chunks and
-//          offsets and the ticket (a whole codec ago), the stores of the last
+//   top    one wait for what the last iteration issued: t's input chunks (a
+//          codec ago), the next tile's offsets, the stores of the last
 //          iteration.  P::stage_in()
 //          -- t's chunks into the LDS stage -- then the loads of the next
-//          tile's input, of the offsets of the tile after it and the next
-//          ticket, and the older pending tile's look-back polls: all of them
-//          have the whole codec to land
+//          tile's input, the claim of the tile after it, and the older
+//          pending tile's look-back polls: all of them have the whole codec
+//          to land
 //   codec  P::prepare() (the encoder's byte-parallel pass over the stage),
 //          P::codec() -- LDS only -- per-lane output size (+ status)
 //   scan   wave scan -> tile-local offsets, tile total; publish the tile
 //          aggregate and add it to the super accumulator (LookBack::start)
 //   emit   P::emit() -- compacted output of t into the LDS out stage
-//   flush  one wait (the polls, a codec and an emit ago, and t's super
-//          add); publish t's super tile's aggregate if t's add completed it;
-//          resolve the older pending tile's look-back and store its output
-//          (registers)
+//   flush  one wait (the polls and the claim, a codec and an emit ago, and
+//          t's super add); the claimed tile's offsets loads; publish t's
+//          super tile's aggregate if t's add completed it; resolve the older
+//          pending tile's look-back and store its output (registers)
 //   gather t's output from the out stage into the freed registers (TileOut)
 //
 // P::kDepth tiles are pending at a time, all holding their output in
@@ -33,8 +33,10 @@
 // the look-backs of the tiles after those: the deeper the pipeline, the more
 // slack before such a delay propagates.)
 //
-// Tiles whose input or output does not fit the stages are coded eagerly by
-// P::slow_tile() (out of line) after the pending tiles have been flushed.
+// Tiles whose input or output does not fit the stages are big tiles: coded
+// in staged units into a global slot and pending like any other (full
+// kernels, P::kBig), or by P::slow_tile() out of line after the pending
+// tiles have been flushed (lean kernels, and a big tile past its slot).
 #pragma once
 
 #include "qhuff_kernels.h"
@@ -426,25 +428,12 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     // tile is always coded (tickets of a group are handed out in order, so
     // once tn is past the end every later claim is too)
     const uint32_t kNone = 0xffffffffu;
-    // late: the third and fourth tickets are claimed by the wave together,
-    // at the first iteration's top, and read after its codec (a burst of
-    // ~3,000 returning adds on 8 counters takes microseconds); that
-    // iteration loads the third tile's offsets then.  Tickets claimed by the
-    // workgroup in the prologue instead hand each workgroup a third tile
-    // ahead of other workgroups' first ones, whose first flush then waits on
-    // the slowest of those third tiles (profiles/r03_u, r04_r: look-back
-    // 3.7 us at the median).  (Claimed in the prologue, after the first
-    // loads, the claim was waited for at the loop's entry: the compiler's
-    // vmcnt(0) for its result's copy, r04_r.)
-    const bool late = tn < nt && k1 != kClaimNow && k2 == kClaimNow;
-    uint32_t kq = tn < nt ? (k2 == kClaimNow ? 0u : k2) : kNone;
-    if (tn < nt && k2 == kClaimNow && !late)
-        kq = tk.claim(c);
+    // the ticket of the third iteration when the workgroup claimed it
+    uint32_t kpre = tn < nt ? k2 : kNone;
     mid();
     Span sp_cur = tile_span(in, o_cur.first(), o_cur.last(), P::kInCap);
     Chunks<P::kNch> ch;
     ch.load(sp_cur);
-    uint32_t kq4 = 0;                        // (late) the third ticket
 
     // Tiles come from in-order tickets claimed two iterations ahead (one
     // claim per wave per iteration), so the order in which a wave claims
@@ -483,28 +472,29 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         // from 1.8k to 0.3k cycles but the kernels did not get faster (enc
         // 65.6 / dec 68.7 vs 65.3 / 68.3 us, interleaved A/B, profiles/r02_g)
         // -- the waves then wait longer in their look-backs.
-        const bool defer = late && it == 0;  // (wave-uniform)
         wait_vm_all();
         prof_stamp(c, it, 1);
         if (sp_cur.staged)
             pol.stage_in(ch, sp_cur, o_cur);
         wave_sync();
         // loads for the next tiles, a whole codec ahead of their use: input
-        // of tn, offsets of the ticketed tile after it, the next ticket; the
-        // oldest pending tile's look-back polls
-        uint32_t tnn = kNone;
-        if (!defer)
-            tnn = tn < nt ? tk.tile_of(kq) : kNone;
+        // of tn, the ticket of the tile after it (read after the codec, when
+        // its offsets are loaded: they land by the next top); the oldest
+        // pending tile's look-back polls.  A tile is thus claimed two
+        // iterations before it is coded (three until round 4: the ticket a
+        // whole iteration ahead of its offsets load), which matters at the
+        // end of a batch: the last tiles go to whichever waves claim them,
+        // and the slowest waves then hold them longest.
         const Span sp_nxt = tile_span(in, o_nxt.first(), o_nxt.last(), P::kInCap);
         ch.load(sp_nxt);
-        if (!defer)
+        uint32_t kq = kNone;
+        if (kpre != kClaimNow)
         {
-            const uint32_t tz = clamp(tnn);
-            o_nn.load(in_off, (uint64_t) tz * TS, cnt_of(tz));
-            kq = tnn < nt ? tk.claim(c) : kNone;
+            kq = kpre;                       // (the prologue's third ticket)
+            kpre = kClaimNow;
         }
-        else
-            kq4 = tk.claim(c, 2);            // third and fourth tickets
+        else if (tn < nt)
+            kq = tk.claim(c);
         LookBack lbo;                        // the oldest pending tile's
         if (pend[0].valid)
         {
@@ -612,13 +602,11 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         // the polls (a codec and an emit ago); resolve + store the oldest
         wait_vm_all();
         prof_stamp(c, it, 4);
-        if (defer)
+        // the ticket has landed: the tile after tn, and its offsets
+        const uint32_t tnn = tn < nt ? tk.tile_of(kq) : kNone;
         {
-            // the late tickets have landed: the third tile's offsets now
-            tnn = tk.tile_of(kq4);
             const uint32_t tz = clamp(tnn);
             o_nn.load(in_off, (uint64_t) tz * TS, cnt_of(tz));
-            kq = tnn < nt ? kq4 + 1 : kNone;
         }
         // t's add has returned with the polls: publish its super tile's
         // aggregate if that add completed it -- here, an emit after the add,
