@@ -484,6 +484,15 @@ flag_inc(uint64_t f)
     return ((f >> 40) & 3) == 2;
 }
 
+// s_sleep between look-back polls after the fourth (x 64 cycles): waits
+// that long are for a slow tile (the drain at a batch's end), where the
+// polls of ~3,000 waves compete with the last codecs' own traffic (with the
+// re-polls of invalid flags only: encode -1.5 ... -1.8 %, decode -0.1 ...
+// -1.2 %, profiles/r04_y)
+#ifndef QH_SPIN_BACKOFF
+#define QH_SPIN_BACKOFF 8
+#endif
+
 struct LookBack
 {
     uint32_t tile, s;
@@ -585,6 +594,11 @@ struct LookBack
                 raise_error(c, kErrSpin);
             return false;
         }
+#if QH_SPIN_BACKOFF
+        if (*spins > 4)
+            __builtin_amdgcn_s_sleep(QH_SPIN_BACKOFF);
+        else
+#endif
         __builtin_amdgcn_s_sleep(2);
         return true;
     }
@@ -620,7 +634,13 @@ struct LookBack
                 done = true;
                 break;
             }
-            ft = poll_tile(c);
+            // re-poll only the flags not yet valid: an aggregate is final
+            // (a valid flag turning inclusive only shortens the sum), and a
+            // wave waiting for a slow tile -- every wave in the drain at the
+            // end of a batch -- then reads one or two cache lines a poll,
+            // not the window's eight
+            if (!v)
+                ft = poll_tile(c);
         }
         const uint32_t spins1 = spins;
         uint32_t extra = 0;                          // windows past the two
@@ -646,7 +666,8 @@ struct LookBack
             }
             if (!spin(c, &spins))
                 break;
-            fs = poll_super(c, back);
+            if (!v)                                  // (as above)
+                fs = poll_super(c, back);
         }
         // Every poll has been consumed, so nothing is outstanding here but
         // the compiler cannot see that the re-poll loads (whose registers the
