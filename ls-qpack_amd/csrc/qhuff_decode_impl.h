@@ -677,15 +677,20 @@ bm_count(const QH_LDS uint32_t *bm, uint32_t r0, uint32_t r1)
 // bytes [rs, re) of the stage, its arena slot at arena + slot) with the whole
 // wave at once: string j gets max(1, bits_j / S) segments of S bits (lanes
 // in string order; S a multiple of 32, >= kSegMin, small enough that the
-// segments fit 64 lanes), its bitmap at word bmw of bms (zeroed here, bits_j
-// / 32 + 2 words) -- A, B, the counts and W as above, each lane on its own
-// string.  sink: kCoopDummy bytes.  Returns, in lane j, string j's output
+// segments fit 64 lanes), its bitmap (bits_j / 32 + 2 words, zeroed here)
+// in its own arena slot, which W overwrites only after the counts: a slot
+// holds 8/5 of the string's bytes, the bitmap 1/4 + 8 -- so any number of
+// long strings fit, however full the arena (round 4 first put the bitmaps
+// above the slots, where two 1,105-byte strings of a full tile did not
+// fit and fell back to one lane each: 200k-cycle tiles on the QIF corpus)
+// -- A, B, the counts and W as above, each lane on its own string.  sink:
+// kCoopDummy bytes.  Returns, in lane j, string j's output
 // length, or -1 when its own lane must decode it (an invalid string, or any
 // disagreement); 0 elsewhere.
 __device__ __forceinline__ int
 coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
             uint32_t re, uint32_t slot, QH_LDS uint8_t *arena,
-            QH_LDS uint32_t *bms, QH_LDS uint8_t *sink,
+            QH_LDS uint8_t *sink,
             const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
             const Coord *pc = nullptr)
 {
@@ -711,9 +716,6 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
     S = S > kSegMin ? S : kSegMin;
     const uint32_t ns = mine ? (nb / S > 0 ? nb / S : 1u) : 0u;
     const uint32_t g = all_lanes(wave_incl_scan(ns)) - ns;   // first segment
-    const uint32_t wds = mine ? nb / 32 + 2 : 0u;
-    const uint32_t wincl = all_lanes(wave_incl_scan(wds));
-    const uint32_t nwords = read_lane(wincl, 63);
     // this lane's string j and segment q
     uint32_t j = lane, gj = 0, nsj = 0;
     for (uint64_t m = coop; m; m &= m - 1)
@@ -730,16 +732,23 @@ coop_decode(const QH_LDS uint32_t *src, uint64_t coop, uint32_t rs,
     const uint32_t rsj = all_lanes((uint32_t) __shfl((int) rs, (int) j, 64));
     const uint32_t rej = all_lanes((uint32_t) __shfl((int) re, (int) j, 64));
     const uint32_t slj = all_lanes((uint32_t) __shfl((int) slot, (int) j, 64));
-    const uint32_t bmj = all_lanes(
-        (uint32_t) __shfl((int) (wincl - wds), (int) j, 64));
     const uint32_t b0 = act ? 8 * rsj : 0u;
     const uint32_t b1 = act ? 8 * rej : 0u;
     QH_LDS uint8_t *sl = arena + slj;
-    QH_LDS uint32_t *bm = bms + bmj;
+    QH_LDS uint32_t *bm = (QH_LDS uint32_t *) (arena + ((slj + 3) & ~3u));
     const uint32_t s = act ? b0 + q * S : 0u;
     const uint32_t stop = !act ? 0u : q + 1 < nsj ? s + S : b1;
-    for (uint32_t i = lane; i < nwords; i += 64)
-        bms[i] = 0;
+    {
+        // each segment's lane zeroes its own words (S is a multiple of 32),
+        // the last one the string's two spare words too
+        const uint32_t wb = act ? (s - b0) >> 5 : 0u;
+        const uint32_t we = !act ? 0u
+                          : q + 1 < nsj ? (stop - b0) >> 5 : (b1 - b0) / 32 + 2;
+        const uint32_t K = wave_max_dpp(we - wb);
+        for (uint32_t k = 0; k < K; ++k)
+            if (wb + k < we)
+                bm[wb + k] = 0;
+    }
     wave_sync();
     // A: guessed walks, marking
     uint32_t E = s, C = 0, h = 0;
@@ -1045,17 +1054,10 @@ struct DecPolicyT
         const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
         // the slots end below kVarArenaBytes - slack + 1 for this span; the
         // bitmap (hl / 4 + 2 words) and the sinks go above them
-        const uint32_t slots_end =
-            2 * kDecTS + (uint32_t) ((8ull * (read_lane(to.o1, cnt - 1) - A)) / 5)
-            + 2;
-        // candidates in lane order while their bitmaps fit (at most 48)
+        // (at most 48 cooperative strings: at least 16 lanes for segments)
         hint = !fixed && __builtin_amdgcn_ballot_w64(valid & (hl > kCoopMin));
         const bool cand = kCoop && !fixed && valid && hl > kCoopMin;
-        const uint32_t bmb = cand ? 4 * (hl / 4 + 2) : 0u;
-        const uint32_t bm0 = (slots_end + 3) & ~3u;
-        const uint32_t bmi = all_lanes(wave_incl_scan(bmb));
-        const bool lng = cand & (bm0 + bmi + kCoopDummy <= (uint32_t) kArenaBytes);
-        coop = __builtin_amdgcn_ballot_w64(lng);
+        coop = __builtin_amdgcn_ballot_w64(cand);
         if (__builtin_popcountll(coop) > 48)
             coop = 0;
         const bool mine = (coop >> lane) & 1;
@@ -1078,13 +1080,8 @@ struct DecPolicyT
                                                uint32_t *sz, uint32_t *st)
     {
         const uint32_t lane = lane_id();
-        const uint32_t A = read_lane(to.o0, lo);
         const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
         const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
-        const uint32_t slots_end =
-            2 * kDecTS + (uint32_t) ((8ull * (read_lane(to.o1, cnt - 1) - A)) / 5)
-            + 2;
-        const uint32_t bm0 = (slots_end + 3) & ~3u;
         const bool mine = (coop >> lane) & 1;
 #ifdef QH_COOP_DEBUG
         bool dbg_fb = false;
@@ -1092,7 +1089,6 @@ struct DecPolicyT
         int r = 0;
         const int rc = coop_decode(
             wv->in, coop, rs, re, slot0, wv->arena,
-            (QH_LDS uint32_t *) (wv->arena + bm0),
             wv->arena + kArenaBytes - kCoopDummy, sm->win, sm->sorted
 #ifdef QHUFF_PROFILE
             , pc
