@@ -7,7 +7,8 @@ kernel times for encode and decode of the bench workload (1,048,576 token
 strings, 8-64 B), or with WORKLOAD=corpus / alphabet_c of bench.py's
 real-workload legs (qhuff/workload.py).
 
-usage: [WORKLOAD=...] python tools/ab_inproc.py LIB_A LIB_B [rounds] [per_block]"""
+usage: [WORKLOAD=...] python tools/ab_inproc.py LIB_A LIB_B [rounds] [per_block]
+(LIB[@VAR=VALUE,...]: knobs set while that context is opened)"""
 import ctypes as C
 import json
 import os
@@ -18,7 +19,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ls-qpack_amd"))
 
 
-def load(path):
+def load(spec):
+    # LIB[@VAR=VALUE[,VAR=VALUE...]]: the variables are set while the
+    # context is opened (qhuff_open reads its knobs then), so one library
+    # can be A/B-ed against itself with other launch knobs
+    path, _, envs = spec.partition("@")
     L = C.CDLL(os.path.abspath(path))
     vp = C.c_void_p
     L.qhuff_open.restype = C.c_int
@@ -29,7 +34,17 @@ def load(path):
     L.qhuff_decode_batch.restype = C.c_int
     L.qhuff_decode_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp, vp]
     ctx = C.c_void_p()
+    saved = {}
+    for kv in filter(None, envs.split(",")):
+        k, _, v = kv.partition("=")
+        saved[k] = os.environ.get(k)
+        os.environ[k] = v
     assert L.qhuff_open(0, C.byref(ctx)) == 0
+    for k, v in saved.items():
+        if v is None:
+            del os.environ[k]
+        else:
+            os.environ[k] = v
     try:
         L.qhuff_timing_enable.argtypes = [vp, C.c_int]
         L.qhuff_timing_read.argtypes = [vp, vp, vp, C.c_uint32]
