@@ -46,8 +46,9 @@ extern "C" {
  *      5-argument qhuff_huff_decode, which is unchanged
  *   3  the low-latency service (qhuff_svc_*) and, in qhuff_lsqpack.h,
  *      qhuff_lsqpack_set_context
- *   4  launch timing (qhuff_timing_enable / qhuff_timing_read) */
-#define QHUFF_ABI_VERSION 4
+ *   4  launch timing (qhuff_timing_enable / qhuff_timing_read)
+ *   5  qhuff_kernel_variant (which kernel variant the last launch ran) */
+#define QHUFF_ABI_VERSION 5
 
 /* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
 int qhuff_abi_version(void);
@@ -372,6 +373,17 @@ uint64_t qhuff_profile_read(qhuff_ctx *ctx, uint64_t *dst, uint64_t max_words);
 #define QHUFF_KIND_HASH   2
 int qhuff_timing_enable(qhuff_ctx *ctx, int on);
 int qhuff_timing_read(qhuff_ctx *ctx, uint32_t *kind, double *us, uint32_t max);
+
+/* Kernel variants.  Encode and decode each have a lean kernel and a full
+ * one that also carries the big-tile slots and the cooperative long-string
+ * decode; by default (QHUFF_KERNELS=auto) a context launches the lean one
+ * until a launch of that kind reports such tiles, then the full one until
+ * 8 launches have been seen to run without any (QHUFF_KERNELS=lean|full
+ * pins one).  Returns 1 if the context's last launch of `kind`
+ * (QHUFF_KIND_ENCODE / QHUFF_KIND_DECODE) ran the full kernel, 0 if the
+ * lean one or none yet, QHUFF_EINVAL otherwise.  Diagnostic: the output
+ * bytes are the same either way. */
+int qhuff_kernel_variant(qhuff_ctx *ctx, int kind);
 
 /* ---- multi-GPU sharding helpers (host arithmetic only) ----------------
  * Byte-balanced contiguous partition of a batch into g shards: writes

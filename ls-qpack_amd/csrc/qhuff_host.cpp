@@ -163,6 +163,7 @@ struct qhuff_ctx
     bool full[2];
     uint32_t calm[2];
     uint32_t seen[2];                    // rare_host[2 kind + 1] last read
+    bool last_full[2];                   // variant of the last launch
     int kernels;                         // QHUFF_KERNELS: 0 auto, 1 lean,
                                          // 2 full
     unsigned long long *prof;            // QHUFF_PROFILE builds: stamp buffer
@@ -681,7 +682,7 @@ pick_full(qhuff_ctx *c, int kind, Coord *k)
 {
     k->rare = c->rare_dev + 2 * kind;
     if (c->kernels)
-        return c->kernels == 2;
+        return c->last_full[kind] = c->kernels == 2;
     volatile uint32_t *r = c->rare_host + 2 * kind;
     if (r[0])
     {
@@ -700,7 +701,15 @@ pick_full(qhuff_ctx *c, int kind, Coord *k)
                 c->full[kind] = false;
         }
     }
-    return c->full[kind];
+    return c->last_full[kind] = c->full[kind];
+}
+
+extern "C" int
+qhuff_kernel_variant(qhuff_ctx *c, int kind)
+{
+    if (!c || (kind != QHUFF_KIND_ENCODE && kind != QHUFF_KIND_DECODE))
+        return QHUFF_EINVAL;
+    return c->last_full[kind] ? 1 : 0;
 }
 
 extern "C" int

@@ -35,7 +35,7 @@ EXPORTS = (
     "qhuff_frame_literal", "qhuff_xxh32_headers_host",
     "qhuff_svc_open", "qhuff_svc_close", "qhuff_svc_encode",
     "qhuff_svc_decode", "qhuff_svc_stats",
-    "qhuff_timing_enable", "qhuff_timing_read",
+    "qhuff_timing_enable", "qhuff_timing_read", "qhuff_kernel_variant",
     # include/qhuff_lsqpack.h
     "qhuff_lsqpack_enc_enc_str", "qhuff_lsqpack_huff_decode",
     "qhuff_lsqpack_set_decode_full", "qhuff_lsqpack_set_device",
@@ -192,6 +192,8 @@ def lib():
                                       C.POINTER(C.c_uint64)]
         L.qhuff_timing_enable.restype = C.c_int
         L.qhuff_timing_enable.argtypes = [vp, C.c_int]
+        L.qhuff_kernel_variant.restype = C.c_int
+        L.qhuff_kernel_variant.argtypes = [vp, C.c_int]
         L.qhuff_timing_read.restype = C.c_int
         L.qhuff_timing_read.argtypes = [vp, u32p, C.POINTER(C.c_double),
                                         C.c_uint32]
@@ -361,6 +363,14 @@ class Codec:
         its dispatch's own start / stop timestamps."""
         self._check(lib().qhuff_timing_enable(self._ctx, 1 if on else 0),
                     "qhuff_timing_enable")
+
+    def kernel_variant(self, kind):
+        """qhuff_kernel_variant: 1 if the last launch of kind (KIND_ENCODE /
+        KIND_DECODE) ran the full kernel, 0 for the lean one."""
+        r = lib().qhuff_kernel_variant(self._ctx, kind)
+        if r < 0:
+            self._check(r, "qhuff_kernel_variant")
+        return r
 
     def timing_read(self, max_launches=TIMING_SLOTS):
         """qhuff_timing_read -> list of (kind, microseconds) of the launches

@@ -397,6 +397,48 @@ def test_kernel_variants(kernels):
         c.close()
 
 
+def test_kernel_variant_switch():
+    """QHUFF_KERNELS=auto (qhuff_host.cpp pick_full): token batches run the
+    lean kernel; a batch with big tiles reports them and the next launch of
+    that kind runs the full one; after 8 launches seen to run without such
+    tiles the lean one again -- counted on launches that ran, so a burst of
+    issued launches does not flip it back (each launch here is synchronised,
+    as the slowest case).  Outputs checked against the oracle throughout."""
+    import qhuff
+    if os.environ.get("QHUFF_KERNELS"):
+        pytest.skip("QHUFF_KERNELS pins the variant")
+    rng = random.Random(11)
+    big = []
+    for t in range(40):
+        tile = rand_strings(rng, 63, ALPHAS["token"], 0, 20) \
+            + rand_strings(rng, 1, ALPHAS["token"], 3200, 5000)
+        big += tile
+    bdata, boff = pack(big)
+    bh, bho = O.encode_batch(bdata, boff, 0)
+    sdata, soff = qhuff.synth_batch(1 << 14, seed=3)
+    sh, sho = O.encode_batch(sdata, soff, 0)
+    c = qhuff.Codec(0)
+    try:
+        E, D = qhuff.KIND_ENCODE, qhuff.KIND_DECODE
+        check_encode(c, sdata, soff, 0)
+        check_decode(c, sh, sho)
+        assert (c.kernel_variant(E), c.kernel_variant(D)) == (0, 0)
+        check_encode(c, bdata, boff, 0)          # lean; reports big tiles
+        check_decode(c, bh, bho)
+        assert (c.kernel_variant(E), c.kernel_variant(D)) == (0, 0)
+        check_encode(c, bdata, boff, 0)
+        check_decode(c, bh, bho)
+        assert (c.kernel_variant(E), c.kernel_variant(D)) == (1, 1)
+        seen = []
+        for _ in range(12):
+            check_encode(c, sdata, soff, 0)
+            check_decode(c, sh, sho)
+            seen.append((c.kernel_variant(E), c.kernel_variant(D)))
+        assert seen[0] == (1, 1) and seen[-1] == (0, 0), seen
+    finally:
+        c.close()
+
+
 def _launch_shape_check(c, n, seed):
     import qhuff
     data, off = qhuff.synth_batch(n, seed=seed)
