@@ -1,3 +1,5 @@
+# experiment record (profiles/r04_tune): the variant libraries were built with
+# make -C ls-qpack_amd OUT=libqhuff_<v>.so OBJDIR=build_<v> DEFS=-DQH_SPIN_BACKOFF=4|16 / -DQH_TAIL_STOP=5|7
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 o=gpurun_out/r04_tune; mkdir -p $o
 A=ls-qpack_amd
