@@ -19,11 +19,11 @@
 #define QH_ENC_DEPTH 3
 #endif
 
-// the dense pass's code table in 32 copies, copy c on LDS bank c, lane l
-// reading copy l % 32 (dense_pass): the 64 lookups of a wave are bank-
-// conflict-free (one copy: text bytes hit a few dozen entries of a 1 KB
-// table, several to a bank).  32 KB of LDS, which the batch kernel has
-// free; the service kernel keeps one copy.
+// QH_MT_REP 1: the dense pass's code table in 32 copies, copy c on LDS bank
+// c, lane l reading copy l % 32 (dense_pass): the 64 lookups of a wave are
+// bank-conflict-free (one copy: text bytes hit a few dozen entries of a
+// 1 KB table, several to a bank), for 32 KB of LDS.  Off: with the round-4
+// dense pass (codes of any length) it measured slower in same-box pairs.
 #ifndef QH_MT_REP
 #define QH_MT_REP 0
 #endif
