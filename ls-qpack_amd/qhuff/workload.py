@@ -13,8 +13,8 @@
   qhuff_pipeline.h / qhuff_decode_impl.h), decode tiles whose arena slots are
   placed by input offset (a string above kFixMaxLen Huffman bytes), decode
   tiles with a string the whole wave decodes (above kCoopMin Huffman bytes,
-  its bitmap fitting past the arena slots: qhuff_decode_impl.h
-  coop_decode), encode tiles that fall back from the dense stream to
+  its bitmap in its own arena slot: qhuff_decode_impl.h coop_decode),
+  encode tiles that fall back from the dense stream to
   per-string packing (the span's codes overflow the dense stream,
   qhuff_encode_impl.h dense_pass) and encode tiles with a payload the whole
   wave copies (above kEncCoopBits dense bits).
@@ -50,14 +50,12 @@ QIF_NAMES = ("fb-req.qif", "fb-resp.qif", "long-codes.qif", "netbsd.qif")
 LONG_CODE_BYTES = bytes([1, 2, 6, 92, 141])
 
 # kernel constants the shares follow (qhuff_pipeline.h kStageCap,
-# qhuff_decode_impl.h kFixMaxLen / kArenaBytes / kCoopMin / kCoopDummy,
+# qhuff_decode_impl.h kFixMaxLen / kCoopMin,
 # qhuff_encode_impl.h kDenseBits / kEncCoopBits)
 STAGE = 3072
 TILE = 64
 FIX_MAX_LEN = (5 * (108 - 1)) // 8
-ARENA = 64 * 108
 COOP_MIN = 128
-COOP_DUMMY = 64
 DENSE_BITS = 32 * (STAGE // 4 + 4 - 2)
 ENC_COOP_BITS = 1024
 
@@ -127,13 +125,10 @@ def tile_shares(data, off, hoff):
     hl = np.diff(hoff)
     max_hl = np.maximum.reduceat(hl, t0) if len(hl) else np.zeros(nt, np.int64)
     var_arena = dec_fast & (max_hl > FIX_MAX_LEN)
-    # a cooperative string: above COOP_MIN, its bitmap past the slots
-    slots_end = 2 * TILE + (8 * (b - a)) // 5 + 2
-    coop_ok = (hl > COOP_MIN) & (np.repeat(slots_end, t1 - t0)
-                                 + 4 * (hl // 4 + 2) + COOP_DUMMY <= ARENA)
-    any_coop = (np.maximum.reduceat(coop_ok.astype(np.int64), t0) > 0
-                if len(hl) else np.zeros(nt, bool))
-    coop = var_arena & any_coop
+    # a cooperative string: above COOP_MIN Huffman bytes (its bitmap lives
+    # in its own arena slot, qhuff_decode_impl.h coop_decode), in a staged
+    # tile -- fast, or big and staged whole
+    coop = dec_staged & (max_hl > COOP_MIN)
     # ---- encode tiles (payload mode) ----
     ea, eb = off[t0], off[t1]
     epa, epb = _span(ea, eb)
