@@ -439,6 +439,31 @@ def test_kernel_variant_switch():
         c.close()
 
 
+def test_small_grid_long_runs():
+    """A grid of a few workgroups (QHUFF_GRID_PCT=4: ~10 of 256) over 4,096
+    tiles: each wave codes ~34 tiles, so the ticket claims two iterations
+    ahead, the youngest waves' claim stop and the pending-tile ring run
+    through many rounds (qhuff_pipeline.h tile_pipeline)."""
+    import qhuff
+    old = os.environ.get("QHUFF_GRID_PCT")
+    os.environ["QHUFF_GRID_PCT"] = "4"
+    try:
+        c = qhuff.Codec(0)
+    finally:
+        if old is None:
+            del os.environ["QHUFF_GRID_PCT"]
+        else:
+            os.environ["QHUFF_GRID_PCT"] = old
+    try:
+        data, off = qhuff.synth_batch(1 << 18, seed=21)
+        g_out, g_off = check_encode(c, data, off, 0)
+        out, oo, st = check_decode(c, g_out, g_off)
+        assert not st.any() and np.array_equal(out, data)
+        assert c.device_error() == 0
+    finally:
+        c.close()
+
+
 def _launch_shape_check(c, n, seed):
     import qhuff
     data, off = qhuff.synth_batch(n, seed=seed)
