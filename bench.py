@@ -75,6 +75,10 @@ def parse():
                          "`value`)")
     ap.add_argument("--probe-launch", action="store_true",
                     help=argparse.SUPPRESS)   # tests: ranks meet, no GPU
+    ap.add_argument("--time-every", type=int, default=10,
+                    help="time every k-th encode / decode launch of the timed "
+                         "region (dispatch-stamped events; each timed launch "
+                         "adds ~4.6 us of queue time to its step)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
                                                   "pmc_latest.json"),
                     help="PMC traffic summary (tools/pmc_summary.py)")
@@ -291,12 +295,14 @@ def main():
               and bool((d_st[0] == 0).all())
               and torch.equal(d_ooff[0], d_off[0]))
 
-    # kernel durations for the roofline: every launch of the timed region
-    # carries a HIP event pair stamped by its own dispatch (qhuff_timing_*:
-    # hipExtLaunchKernel's start / stop events -- the kernel's device time,
-    # as rocprofv3's kernel trace measures it, and no timing packets between
-    # the launches); the last QHUFF_TIMING_SLOTS launches are read back
-    codec.timing(True)
+    # kernel durations for the roofline: every --time-every-th launch of each
+    # kind in the timed region carries a HIP event pair stamped by its own
+    # dispatch (qhuff_timing_*: hipExtLaunchKernel's start / stop events --
+    # the kernel's device time, as rocprofv3's kernel trace measures it).
+    # Sampled: a timed launch adds ~4.6 us of queue time to its step
+    # (tools/timing_cost.py: 114.8 vs 105.6 us per step with every launch
+    # timed / none, profiles/r04_tc), which would otherwise count in `value`
+    codec.timing(True, every=args.time_every)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -355,11 +361,11 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": kname, "kernel_us": round(kms * 1e3, 2),
             "alg_bytes": alg,
-            "timing": "mean over %d %s launches of the timed region, each "
-                      "dispatched with HIP start/stop events stamped by the "
-                      "dispatch itself (hipExtLaunchKernel)"
+            "timing": "mean over %d %s launches of the timed region (every "
+                      "%d-th), each dispatched with HIP start/stop events "
+                      "stamped by the dispatch itself (hipExtLaunchKernel)"
                       % (len(dec_t if kname == "qhuff_decode_kernel" else enc_t),
-                         kname)}
+                         kname, max(1, args.time_every))}
     if pmc_src:
         roof["traffic_source"] = pmc_src
 

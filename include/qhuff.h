@@ -47,7 +47,8 @@ extern "C" {
  *   3  the low-latency service (qhuff_svc_*) and, in qhuff_lsqpack.h,
  *      qhuff_lsqpack_set_context
  *   4  launch timing (qhuff_timing_enable / qhuff_timing_read)
- *   5  qhuff_kernel_variant (which kernel variant the last launch ran) */
+ *   5  qhuff_kernel_variant (which kernel variant the last launch ran);
+ *      qhuff_timing_enable(ctx, k > 1) samples every k-th launch */
 #define QHUFF_ABI_VERSION 5
 
 /* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
@@ -365,7 +366,9 @@ uint64_t qhuff_profile_read(qhuff_ctx *ctx, uint64_t *dst, uint64_t max_words);
  * QHUFF_TIMING_SLOTS launches.  qhuff_timing_read waits for them and
  * returns, oldest first, the launches timed since timing was enabled or
  * last read (at most `max`, the most recent ones): kind[i] (QHUFF_KIND_*)
- * and us[i], microseconds.  qhuff_timing_enable(ctx, 0) turns it off.
+ * and us[i], microseconds.  qhuff_timing_enable(ctx, 0) turns it off;
+ * `on` = k > 1 (ABI 5) times only every k-th launch of each kind, counted
+ * from the call (a timed launch costs a few microseconds of queue time).
  * Return QHUFF_OK / the count, or QHUFF_E*. */
 #define QHUFF_TIMING_SLOTS 256
 #define QHUFF_KIND_ENCODE 0

@@ -358,11 +358,12 @@ class Codec:
         (0 = none, 1 = a look-back wait gave up)."""
         return int(lib().qhuff_device_error(self._ctx))
 
-    def timing(self, on=True):
-        """qhuff_timing_enable: time every later launch of this context by
-        its dispatch's own start / stop timestamps."""
-        self._check(lib().qhuff_timing_enable(self._ctx, 1 if on else 0),
-                    "qhuff_timing_enable")
+    def timing(self, on=True, every=1):
+        """qhuff_timing_enable: time every later launch of this context (or
+        every `every`-th of each kind) by its dispatch's own start / stop
+        timestamps."""
+        self._check(lib().qhuff_timing_enable(
+            self._ctx, max(1, int(every)) if on else 0), "qhuff_timing_enable")
 
     def kernel_variant(self, kind):
         """qhuff_kernel_variant: 1 if the last launch of kind (KIND_ENCODE /
