@@ -464,6 +464,32 @@ def test_small_grid_long_runs():
         c.close()
 
 
+def test_launch_timing(codec):
+    """qhuff_timing_enable / qhuff_timing_read (ABIs 4-5): every launch, or
+    every k-th of each kind, comes back with its kind and a positive device
+    time; the outputs are the same either way."""
+    import qhuff
+    data, off = qhuff.synth_batch(1 << 14, seed=5)
+    codec.timing(True)
+    check_encode(codec, data, off, 0)
+    check_encode(codec, data, off, 0)
+    t = codec.timing_read()
+    assert [k for k, _ in t] == [qhuff.KIND_ENCODE] * 2
+    assert all(u > 0 for _, u in t)
+    codec.timing(True, every=3)
+    h, ho = O.encode_batch(data, off, 0)
+    for _ in range(7):
+        check_encode(codec, data, off, 0)
+        check_decode(codec, h, ho)
+    t = codec.timing_read()
+    codec.timing(False)
+    assert [k for k, _ in t].count(qhuff.KIND_ENCODE) == 3      # 0, 3, 6
+    assert [k for k, _ in t].count(qhuff.KIND_DECODE) == 3
+    assert all(u > 0 for _, u in t)
+    check_encode(codec, data, off, 0)
+    assert codec.timing_read() == []
+
+
 def _launch_shape_check(c, n, seed):
     import qhuff
     data, off = qhuff.synth_batch(n, seed=seed)
