@@ -48,8 +48,11 @@ extern "C" {
  *      qhuff_lsqpack_set_context
  *   4  launch timing (qhuff_timing_enable / qhuff_timing_read)
  *   5  qhuff_kernel_variant (which kernel variant the last launch ran);
- *      qhuff_timing_enable(ctx, k > 1) samples every k-th launch */
-#define QHUFF_ABI_VERSION 5
+ *      qhuff_timing_enable(ctx, k > 1) samples every k-th launch
+ *   6  QHUFF_MAX_STRLEN: qhuff_scan_field_section rejects (QHUFF_EPROTO) a
+ *      literal whose declared length exceeds it; qhuff_decode_literals_ex
+ *      rejects a literal whose decoded length does */
+#define QHUFF_ABI_VERSION 6
 
 /* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
 int qhuff_abi_version(void);
@@ -251,6 +254,13 @@ qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, int src_len,
 #define QHUFF_LIT_NAME   1
 #define QHUFF_LIT_VALUE  2
 
+/* LSXPACK_MAX_STRLEN (lsxpack_header.h:12-13): the longest name or value a
+ * field section may carry.  The reference rejects a field-section literal
+ * whose declared length exceeds it right after the length integer
+ * (lsqpack.c:3682-3685 values, 3769-3772 names) and a decoded one that
+ * outgrows it (header_out_grow_buf, lsqpack.c:3350-3351). */
+#define QHUFF_MAX_STRLEN 65535u
+
 struct qhuff_literal
 {
     uint32_t pos;               /* payload offset: pos_base + offset in buf */
@@ -267,7 +277,9 @@ struct qhuff_literal
 /* One complete encoded field section (prefix + field lines).  Writes up to
  * max_lits literals in wire order and the count to *n_lits.  QHUFF_OK,
  * QHUFF_ETRUNC (ends inside a line), QHUFF_EPROTO (an integer the reference
- * rejects), QHUFF_ERANGE (*n_lits is the count needed). */
+ * rejects, or (ABI 6) a literal length above QHUFF_MAX_STRLEN, reported as
+ * soon as the length is decoded, whether or not its bytes follow),
+ * QHUFF_ERANGE (*n_lits is the count needed). */
 int qhuff_scan_field_section(const uint8_t *buf, size_t len, uint32_t pos_base,
                              struct qhuff_literal *lits, uint32_t max_lits,
                              uint32_t *n_lits);
@@ -293,6 +305,17 @@ int qhuff_decode_literals_host(qhuff_ctx *ctx, const uint8_t *buf,
                                const struct qhuff_literal *lits, uint32_t n,
                                uint8_t *out, uint32_t *out_off,
                                uint8_t *status);
+
+/* (ABI 6) qhuff_decode_literals_host with a length limit: a literal whose
+ * decoded (Huffman) or raw length exceeds max_len gets QHUFF_DEC_ERROR and
+ * 0 bytes.  Field-section literals take max_len = QHUFF_MAX_STRLEN (the
+ * reference's header_out_grow_buf rule, lsqpack.c:3350-3351: a string
+ * never outgrows LSXPACK_MAX_STRLEN); 0 = no limit (encoder-stream literals,
+ * whose bound is the dynamic table's capacity, lsqpack.c:4661-4667). */
+int qhuff_decode_literals_ex(qhuff_ctx *ctx, const uint8_t *buf,
+                             const struct qhuff_literal *lits, uint32_t n,
+                             uint32_t max_len, uint8_t *out, uint32_t *out_off,
+                             uint8_t *status);
 
 /* ---- encoder-side hook ---------------------------
  * lsqpack_enc_enc_str (lsqpack.c:839-876) for a string whose Huffman

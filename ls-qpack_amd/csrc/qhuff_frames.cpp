@@ -86,10 +86,14 @@ struct Sink
 };
 
 // a string literal whose H bit sits just above its N-bit length prefix
-// (the layouts lsqpack_enc_enc_str writes for N = 3, 5, 7, lsqpack.c:839)
+// (the layouts lsqpack_enc_enc_str writes for N = 3, 5, 7, lsqpack.c:839).
+// max_len > 0: a declared length above it is an error as soon as the length
+// is decoded, before the payload is looked for -- the field-section rule
+// (LSXPACK_MAX_STRLEN, lsqpack.c:3682-3685 values, 3769-3772 names; pinned
+// by test/test_header_alloc_clamp.c:108-135).
 int
 literal(Sink &s, const uint8_t **pp, const uint8_t *end, unsigned prefix_bits,
-        unsigned kind, uint32_t instr)
+        unsigned kind, uint32_t instr, uint32_t max_len)
 {
     const uint8_t *p = *pp;
     if (p >= end)
@@ -100,6 +104,8 @@ literal(Sink &s, const uint8_t **pp, const uint8_t *end, unsigned prefix_bits,
     const int r = dec_int24(&p, end, prefix_bits, &len);
     if (r)
         return r;
+    if (max_len && len > max_len)
+        return -2;
     if ((uint64_t) (end - p) < len)
         return -1;
     if (s.n < s.cap)
@@ -139,6 +145,7 @@ qhuff_scan_field_section(const uint8_t *buf, size_t len, uint32_t pos_base,
     *n_lits = 0;
     Sink s{buf, pos_base, lits, max_lits, 0, false};
     const uint8_t *p = buf, *const end = buf + len;
+    const uint32_t max_str = QHUFF_MAX_STRLEN;
     uint64_t v;
     int r;
     // section prefix: Required Insert Count (8-bit prefix), S + Delta Base
@@ -156,13 +163,13 @@ qhuff_scan_field_section(const uint8_t *buf, size_t len, uint32_t pos_base,
         {
             r = dec_int24(&p, end, 4, &idx);
             if (!r)
-                r = literal(s, &p, end, 7, QHUFF_LIT_VALUE, at);
+                r = literal(s, &p, end, 7, QHUFF_LIT_VALUE, at, max_str);
         }
         else if (b & 0x20)                     // 001NHxxx literal name
         {
-            r = literal(s, &p, end, 3, QHUFF_LIT_NAME, at);
+            r = literal(s, &p, end, 3, QHUFF_LIT_NAME, at, max_str);
             if (!r)
-                r = literal(s, &p, end, 7, QHUFF_LIT_VALUE, at);
+                r = literal(s, &p, end, 7, QHUFF_LIT_VALUE, at, max_str);
         }
         else if (b & 0x10)                     // 0001xxxx indexed post-base
             r = dec_int24(&p, end, 4, &idx);
@@ -170,7 +177,7 @@ qhuff_scan_field_section(const uint8_t *buf, size_t len, uint32_t pos_base,
         {
             r = dec_int24(&p, end, 3, &idx);
             if (!r)
-                r = literal(s, &p, end, 7, QHUFF_LIT_VALUE, at);
+                r = literal(s, &p, end, 7, QHUFF_LIT_VALUE, at, max_str);
         }
         if (r)
             return rc_of(r);
@@ -203,13 +210,13 @@ qhuff_scan_encoder_stream(const uint8_t *buf, size_t len, uint32_t pos_base,
         {
             r = dec_int24(&q, end, 6, &v);
             if (!r)
-                r = literal(s, &q, end, 7, QHUFF_LIT_VALUE, at);
+                r = literal(s, &q, end, 7, QHUFF_LIT_VALUE, at, 0);
         }
         else if (b & 0x40)           // 01Hxxxxx insert with literal name
         {
-            r = literal(s, &q, end, 5, QHUFF_LIT_NAME, at);
+            r = literal(s, &q, end, 5, QHUFF_LIT_NAME, at, 0);
             if (!r)
-                r = literal(s, &q, end, 7, QHUFF_LIT_VALUE, at);
+                r = literal(s, &q, end, 7, QHUFF_LIT_VALUE, at, 0);
         }
         else                         // 001xxxxx capacity / 000xxxxx dup
         {

@@ -1574,6 +1574,19 @@ qhuff_decode_literals_host(qhuff_ctx *c, const uint8_t *buf,
                            const struct qhuff_literal *lits, uint32_t n,
                            uint8_t *out, uint32_t *out_off, uint8_t *status)
 {
+    return qhuff_decode_literals_ex(c, buf, lits, n, 0, out, out_off, status);
+}
+
+// max_len > 0: the field-section limit -- a string that decodes (or is
+// declared, raw) longer than LSXPACK_MAX_STRLEN is an error in the
+// reference (header_out_grow_buf, lsqpack.c:3350-3351; 3682-3685,
+// 3769-3772), whatever the kernel's status.
+extern "C" int
+qhuff_decode_literals_ex(qhuff_ctx *c, const uint8_t *buf,
+                         const struct qhuff_literal *lits, uint32_t n,
+                         uint32_t max_len, uint8_t *out, uint32_t *out_off,
+                         uint8_t *status)
+{
     if (!c || !out_off || (n && (!buf || !lits || !out || !status)))
         return QHUFF_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1651,11 +1664,18 @@ qhuff_decode_literals_host(qhuff_ctx *c, const uint8_t *buf,
         if (lits[i].huffman)
         {
             const uint32_t a = doo[k], b = doo[k + 1];
-            status[i] = dst[k];
+            ++k;
+            if (max_len && b - a > max_len)
+            {
+                status[i] = QHUFF_DEC_ERROR;
+                continue;
+            }
+            status[i] = dst[k - 1];
             memcpy(out + o, c->h_stage + o_out + a, b - a);
             o += b - a;
-            ++k;
         }
+        else if (max_len && lits[i].len > max_len)
+            status[i] = QHUFF_DEC_ERROR;
         else
         {
             status[i] = QHUFF_DEC_OK;

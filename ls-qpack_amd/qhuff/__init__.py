@@ -32,6 +32,7 @@ EXPORTS = (
     "qhuff_xxh32_headers", "qhuff_xxh32_batch",
     "qhuff_scan_field_section", "qhuff_scan_encoder_stream",
     "qhuff_literals_bound", "qhuff_decode_literals_host",
+    "qhuff_decode_literals_ex",
     "qhuff_frame_literal", "qhuff_xxh32_headers_host",
     "qhuff_svc_open", "qhuff_svc_close", "qhuff_svc_encode",
     "qhuff_svc_decode", "qhuff_svc_stats",
@@ -45,6 +46,7 @@ EPROTO, ETRUNC = -71, -61
 TIMING_SLOTS = 256                        # QHUFF_TIMING_SLOTS
 KIND_ENCODE, KIND_DECODE, KIND_HASH = 0, 1, 2
 LIT_NAME, LIT_VALUE = 1, 2
+MAX_STRLEN = 65535                        # QHUFF_MAX_STRLEN (LSXPACK_MAX_STRLEN)
 
 XXH_SEED = 39378473                       # LSQPACK_XXH_SEED, lsqpack.c:623
 
@@ -173,6 +175,9 @@ def lib():
         L.qhuff_decode_literals_host.restype = C.c_int
         L.qhuff_decode_literals_host.argtypes = [vp, vp, vp, C.c_uint32, vp,
                                                  u32p, vp]
+        L.qhuff_decode_literals_ex.restype = C.c_int
+        L.qhuff_decode_literals_ex.argtypes = [vp, vp, vp, C.c_uint32,
+                                               C.c_uint32, vp, u32p, vp]
         L.qhuff_xxh32_headers_host.restype = C.c_int
         L.qhuff_xxh32_headers_host.argtypes = [vp, vp, u32p, C.c_uint32,
                                                C.c_uint32, u32p, u32p]
@@ -517,9 +522,11 @@ class Codec:
         self._check(rc, "qhuff_decode_batch_host")
         return out[:out_off[-1]], out_off, status[:n]
 
-    def decode_literals_host(self, buf, lits):
+    def decode_literals_host(self, buf, lits, max_len=None):
         """Decode pre-parsed literals of host buffer buf in one GPU batch ->
-        (list of bytes, status uint8 ndarray)."""
+        (list of bytes, status uint8 ndarray).  max_len (e.g. MAX_STRLEN for
+        field-section literals) calls qhuff_decode_literals_ex: a literal
+        longer than it once decoded is an ERROR."""
         import numpy as np
         n = len(lits)
         arr = (Literal * max(n, 1))(*lits)
@@ -528,9 +535,14 @@ class Codec:
         out = np.zeros(cap, dtype=np.uint8)
         out_off = np.zeros(n + 1, dtype=np.uint32)
         status = np.zeros(max(n, 1), dtype=np.uint8)
-        rc = lib().qhuff_decode_literals_host(self._ctx, _np_ptr(src), arr, n,
-                                              _np_ptr(out), _np_ptr(out_off),
-                                              _np_ptr(status))
+        if max_len is None:
+            rc = lib().qhuff_decode_literals_host(
+                self._ctx, _np_ptr(src), arr, n, _np_ptr(out), _np_ptr(out_off),
+                _np_ptr(status))
+        else:
+            rc = lib().qhuff_decode_literals_ex(
+                self._ctx, _np_ptr(src), arr, n, max_len, _np_ptr(out),
+                _np_ptr(out_off), _np_ptr(status))
         self._check(rc, "qhuff_decode_literals_host")
         return ([out[out_off[i]:out_off[i + 1]].tobytes() for i in range(n)],
                 status[:n])

@@ -13,6 +13,8 @@ Sources (all under /root/reference):
   test/test_read_enc_stream.c tests[] (encoder-stream bytes -> dyn table)
   test/test_qpack.c          header_block_tests[] (headers -> enc/prefix/
                              header-block bytes)
+  test/test_header_alloc_clamp.c  the two over-long-length blocks main()
+                             builds (LSXPACK_MAX_STRLEN clamp, LQRHS_ERROR)
   lsqpack.c                  static_table[] (QPACK static table, data)
   fuzz/input/256.100.1/*     interop-encode output, -t 256 -s 100 -a 1
   test/qifs/*.qif            QIF corpora the streams above were encoded from
@@ -223,6 +225,63 @@ def rel(p):
     return os.path.relpath(p, REF)
 
 
+def hpack_int(first, value, prefix_bits):
+    """RFC 7541 5.1 prefixed integer OR-ed into `first` (the reference's
+    lsqpack_enc_int, lsqpack.c:784-814, with room to spare)."""
+    mask = (1 << prefix_bits) - 1
+    if value < mask:
+        return bytes([first | value])
+    out, value = bytearray([first | mask]), value - mask
+    while value >= 128:
+        out.append(0x80 | (value & 0x7f))
+        value >>= 7
+    out.append(value)
+    return bytes(out)
+
+
+def clamp_cases(path):
+    """The blocks test/test_header_alloc_clamp.c builds in main(): each
+    `Case N` writes bytes with `*p++ = EXPR;` / `*p = EXPR;`, appends
+    `lsqpack_enc_int(p, end, bignum, PREFIX)` and asserts the status of
+    decode_block().  Parsed as text: the statements are evaluated with the
+    initializer evaluator, the integer encoded by hpack_int."""
+    text = open(path, encoding="latin-1").read()
+    big = int(re.search(r"const\s+unsigned\s+bignum\s*=\s*(\d+)\s*;",
+                        text).group(1))
+    cases = []
+    starts = [m.start() for m in re.finditer(r"/\*\s*Case\s+\d+", text)]
+    for k, s in enumerate(starts):
+        e = starts[k + 1] if k + 1 < len(starts) else text.index("printf", s)
+        body = text[s:e]
+        line = text.count("\n", 0, s) + 1
+        title = re.sub(r"\n\s*\*", " ",
+                       re.match(r"/\*\s*(.*?)\*/", body, re.S).group(1))
+        blk = bytearray()
+        stmt = re.compile(r"\*p(\+\+)?\s*=\s*([^;]+);|lsqpack_enc_int\(\s*p\s*,"
+                          r"\s*end\s*,\s*(\w+)\s*,\s*(\d+)\s*\)"
+                          r"|rhs\s*==\s*(\w+)")
+        status, pending = None, None
+        for m in stmt.finditer(body):
+            if m.group(2) is not None:
+                v = evaluate(tokenize(m.group(2), 0))
+                if m.group(1):
+                    blk.append(v & 0xff)
+                else:
+                    pending = v & 0xff
+            elif m.group(3) is not None:
+                assert m.group(3) == "bignum" and pending is not None
+                blk += hpack_int(pending, big, int(m.group(4)))
+                pending = None
+            else:
+                status = m.group(5)
+        assert status and pending is None
+        cases.append({"source": "%s:%d" % (rel(path), line),
+                      "what": " ".join(title.split()),
+                      "block": bytes(blk).hex(), "declared_len": big,
+                      "expect": status})
+    return cases
+
+
 def as_bytes(v, size=None):
     if isinstance(v, (bytes, bytearray)):
         b = bytes(v)
@@ -289,6 +348,12 @@ def main():
                    "prefix": as_bytes(t.get("qhbt_prefix_buf"))[:t["qhbt_prefix_sz"]].hex(),
                    "header": as_bytes(t.get("qhbt_header_buf"))[:t["qhbt_header_sz"]].hex()})
     out["kat_header_blocks.json"] = {"header_blocks": hb}
+
+    f = os.path.join(REF, "test/test_header_alloc_clamp.c")
+    out["kat_header_alloc_clamp.json"] = {
+        "max_strlen": 65535, "max_strlen_source": "lsxpack_header.h:12-13",
+        "clamp_sites": "lsqpack.c:3682-3685, 3769-3772, 3350-3351",
+        "cases": clamp_cases(f)}
 
     f = os.path.join(REF, "lsqpack.c")
     st = []

@@ -36,6 +36,20 @@ def read_int(buf, pos, prefix_bits):
             return v, pos
 
 
+def enc_int(first, value, prefix_bits):
+    """RFC 7541 5.1 prefixed integer OR-ed into the first byte (what
+    lsqpack_enc_int writes, lsqpack.c:784-814) -> bytes."""
+    mask = (1 << prefix_bits) - 1
+    if value < mask:
+        return bytes([first | value])
+    out, value = bytearray([first | mask]), value - mask
+    while value >= 128:
+        out.append(0x80 | (value & 0x7f))
+        value >>= 7
+    out.append(value)
+    return bytes(out)
+
+
 def read_literal(buf, pos, prefix_bits):
     """A string literal whose H bit sits just above an N-bit length prefix.
     Returns a dict with the literal's framing and payload."""
@@ -216,11 +230,18 @@ def dec_int24(buf, pos, prefix_bits):
     return v, pos
 
 
-def _lit(buf, pos, prefix_bits, kind, instr):
+MAX_STRLEN = 65535            # LSXPACK_MAX_STRLEN, lsxpack_header.h:12-13
+
+
+def _lit(buf, pos, prefix_bits, kind, instr, max_len=0):
+    """max_len: the field-section clamp -- a declared length above it fails
+    as soon as it is decoded (lsqpack.c:3682-3685, 3769-3772)."""
     if pos >= len(buf):
         raise Truncated()
     h = (buf[pos] >> prefix_bits) & 1
     n, p = dec_int24(buf, pos, prefix_bits)
+    if max_len and n > max_len:
+        raise ProtoError()
     if p + n > len(buf):
         raise Truncated()
     return (p, n, h, prefix_bits, p - pos, kind, instr), p + n
@@ -244,17 +265,17 @@ def ref_scan_field_section(buf):
                 _, pos = dec_int24(buf, pos, 6)
             elif b & 0x40:                     # literal with name reference
                 _, pos = dec_int24(buf, pos, 4)
-                lit, pos = _lit(buf, pos, 7, LIT_VALUE, at)
+                lit, pos = _lit(buf, pos, 7, LIT_VALUE, at, MAX_STRLEN)
                 lits.append(lit)
             elif b & 0x20:                     # literal with literal name
-                n, pos = _lit(buf, pos, 3, LIT_NAME, at)
-                v, pos = _lit(buf, pos, 7, LIT_VALUE, at)
+                n, pos = _lit(buf, pos, 3, LIT_NAME, at, MAX_STRLEN)
+                v, pos = _lit(buf, pos, 7, LIT_VALUE, at, MAX_STRLEN)
                 lits += [n, v]
             elif b & 0x10:                     # indexed post-base
                 _, pos = dec_int24(buf, pos, 4)
             else:                              # post-base name reference
                 _, pos = dec_int24(buf, pos, 3)
-                lit, pos = _lit(buf, pos, 7, LIT_VALUE, at)
+                lit, pos = _lit(buf, pos, 7, LIT_VALUE, at, MAX_STRLEN)
                 lits.append(lit)
     except Truncated:
         return "trunc", []

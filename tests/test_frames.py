@@ -145,6 +145,74 @@ def test_scan_rejects_like_the_reference():
         == qhuff.EPROTO
 
 
+# ---- LSXPACK_MAX_STRLEN (lsqpack.c:3682-3685, 3769-3772, 3350-3351) --------
+
+def clamp_kat():
+    with open(os.path.join(G, "kat_header_alloc_clamp.json")) as f:
+        return json.load(f)
+
+
+def field_line(first, prefix_bits, payload, huffman=False):
+    """one string literal: H bit above an N-bit prefixed length, then the
+    payload (RFC 9204 4.5.4 / 4.5.6 shapes)"""
+    if huffman:
+        first |= 1 << prefix_bits
+    return Q.enc_int(first, len(payload), prefix_bits) + payload
+
+
+def test_alloc_clamp_kats():
+    """test/test_header_alloc_clamp.c:108-135: an over-long declared value /
+    name length is LQRHS_ERROR right after the length (not 'need more
+    bytes': the payload is absent)."""
+    kat = clamp_kat()
+    assert kat["max_strlen"] == qhuff.MAX_STRLEN == Q.MAX_STRLEN
+    assert len(kat["cases"]) == 2
+    for case in kat["cases"]:
+        assert case["expect"] == "LQRHS_ERROR"
+        blk = bytes.fromhex(case["block"])
+        assert qhuff.scan_field_section(blk)[0] == qhuff.EPROTO, case["source"]
+        assert Q.ref_scan_field_section(blk)[0] == "proto"
+
+
+@pytest.mark.parametrize("shape", ["nameref", "literal_name", "literal_value",
+                                   "postbase"])
+@pytest.mark.parametrize("n", [65535, 65536, 70000])
+def test_alloc_clamp_present_bytes(shape, n):
+    """a literal of n bytes whose payload IS present: accepted up to
+    LSXPACK_MAX_STRLEN, rejected (EPROTO) above it -- round 4 returned OK
+    for a complete 70,000-byte value."""
+    big = b"x" * n
+    if shape == "nameref":           # 01NT + 4-bit static index 0
+        line = b"\x50" + field_line(0, 7, big)
+    elif shape == "literal_name":    # 001NH + 3-bit name length
+        line = field_line(0x20, 3, big) + field_line(0, 7, b"v")
+    elif shape == "literal_value":
+        line = field_line(0x20, 3, b"n") + field_line(0, 7, big)
+    else:                            # 0000N + 3-bit post-base index
+        line = b"\x00" + field_line(0, 7, big)
+    blk = b"\x00\x00" + line
+    rc, lits = qhuff.scan_field_section(blk)
+    want = qhuff.OK if n <= qhuff.MAX_STRLEN else qhuff.EPROTO
+    assert rc == want
+    assert Q.ref_scan_field_section(blk)[0] == ("ok" if rc == qhuff.OK
+                                                 else "proto")
+    if rc == qhuff.OK:
+        assert max(l.len for l in lits) == n
+    # declared, payload absent: still EPROTO above the limit, ETRUNC below
+    rc2 = qhuff.scan_field_section(blk[:-(n // 2)] if shape != "literal_name"
+                                   else blk[:8])[0]
+    assert rc2 == (qhuff.ETRUNC if n <= qhuff.MAX_STRLEN else qhuff.EPROTO)
+
+
+def test_encoder_stream_not_clamped():
+    """the encoder stream has no LSXPACK_MAX_STRLEN rule (its bound is the
+    table capacity, lsqpack.c:4661-4667, which a framing scan does not
+    know): a 70,000-byte value is scanned as a literal"""
+    ins = field_line(0xc0, 6, b"")[:1] + field_line(0, 7, b"y" * 70000)
+    rc, lits, used = qhuff.scan_encoder_stream(ins)
+    assert rc == qhuff.OK and used == len(ins) and lits[0].len == 70000
+
+
 # ---- GPU: all literals of the reference streams in one decode batch ---------
 
 @pytest.fixture(scope="module")
@@ -219,6 +287,41 @@ def test_gpu_decode_literals_with_errors(codec):
             assert o == (want if ost == O.OK else b"")
         else:
             assert st == 0 and o == payload
+
+
+@pytest.mark.gpu
+def test_gpu_decode_clamp(codec):
+    """header_out_grow_buf (lsqpack.c:3350-3351): a field-section string
+    never decodes past LSXPACK_MAX_STRLEN.  65,535 and 65,536 'a's (5-bit
+    code) both fit a 40,960-byte Huffman payload, declared well under the
+    limit: the scan accepts both, the literal decode with
+    max_len = MAX_STRLEN keeps the first and rejects the second, and
+    without a limit (encoder-stream use) decodes both.  The reference's
+    over-long declared lengths (test_header_alloc_clamp.c) never reach the
+    decode: the scan rejects their blocks."""
+    for case in clamp_kat()["cases"]:
+        assert qhuff.scan_field_section(bytes.fromhex(case["block"]))[0] \
+            == qhuff.EPROTO
+    buf, lits = b"", []
+    for n in (65535, 65536, 10, 0):
+        h = O.huffman_enc(b"a" * n)
+        blk = (b"\x00\x00" + field_line(0x20, 3, b"nm")
+               + field_line(0, 7, h, huffman=True))
+        rc, ls = qhuff.scan_field_section(blk, len(buf))
+        assert rc == qhuff.OK
+        buf += blk
+        lits += ls
+    outs, status = codec.decode_literals_host(buf, lits, qhuff.MAX_STRLEN)
+    assert list(status) == [0, 0, 0, 1, 0, 0, 0, 0]
+    assert outs[1] == b"a" * 65535 and outs[3] == b""
+    assert outs[5] == b"a" * 10 and outs[7] == b""
+    outs, status = codec.decode_literals_host(buf, lits)
+    assert not status.any() and outs[3] == b"a" * 65536
+    # a raw literal above the limit (only reachable through hand-made spans)
+    raw = [qhuff.Literal(0, 70000, 0, 7, 2, 0, 0)]
+    outs, status = codec.decode_literals_host(b"z" * 70000, raw,
+                                              qhuff.MAX_STRLEN)
+    assert list(status) == [1] and outs == [b""]
 
 
 @pytest.mark.gpu
