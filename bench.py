@@ -415,7 +415,8 @@ def main():
     work = None
     if args.workloads and rank == 0 and world == 1:
         work = run_workloads(args, np, torch, qhuff, codec, dev, stream, n,
-                             raw_bytes, enc_ms, dec_ms)
+                             raw_bytes, enc_ms, dec_ms,
+                             (d_in[0], d_off[0], d_hin[0], d_hoff[0]))
 
     host = None
     if args.host_path and rank == 0:
@@ -569,19 +570,29 @@ def run_overlap(args, np, torch, qhuff, dev, n, raw, d_in, d_off, e_out,
 
 
 def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
-                  enc_ms_syn, dec_ms_syn):
+                  enc_ms_syn, dec_ms_syn, syn):
     """Real-workload shapes, never `value`: 1M-string
     batches of the reference's QIF corpora (names and values in wire order,
     repeated), of the base64 alphabet and of the long-code alphabet C; each
     encoded and decoded K times with dispatch-stamped timing (kernel device
     time), the round trip checked, and the tile-path shares of each batch
-    (qhuff/workload.py: slow tiles, variable arena slots, encode fallback)."""
+    (qhuff/workload.py: slow tiles, variable arena slots, encode fallback).
+    first_launch_us: each batch's first encode and
+    first decode launch, timed right after 8 token launches of each kind on
+    the same context -- no warm-up on the batch itself (the code objects are
+    loaded by the earlier legs); round 4's history-based kernel choice ran
+    that launch lean, 3.4 ms / 0.7 ms on the corpus."""
     from qhuff import workload as W
     K = 10
     data_dir = os.path.join(ROOT, "tests", "golden", "data")
-    # (the corpus last: after its big tiles the context keeps the full
-    # kernels until 8 launches have run without them -- qhuff_host.cpp
-    # pick_full -- which would time the other batches partly on those)
+    s_in, s_off, s_h, s_hoff = syn
+    s_eo = torch.empty(qhuff.encode_bound(int(s_in.numel()), n, 0),
+                       dtype=torch.uint8, device=dev)
+    s_eoo = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    s_do = torch.empty(qhuff.decode_bound(int(s_h.numel()), n),
+                       dtype=torch.uint8, device=dev)
+    s_doo = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    s_st = torch.empty(n, dtype=torch.uint8, device=dev)
     batches = [
         ("base64", "synthetic U[8,64], base64 alphabet",
          qhuff.synth_batch(n, alphabet=qhuff.BASE64_ALPHABET)),
@@ -610,13 +621,33 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
                          device=dev)
         doo = torch.empty(n + 1, dtype=torch.int32, device=dev)
         st = torch.empty(n, dtype=torch.uint8, device=dev)
-        # warm-up: the first launches pick the kernel variant for this data
-        # (qhuff_host.cpp pick_full) and load it (code objects load at a
-        # kernel's first launch in the process)
-        for _ in range(3):
+        # the first launch of each kind on this batch, after 8 token
+        # launches of each kind (the output is checked with the others')
+        for _ in range(8):
+            codec.encode_into(s_in, s_off, n, 0, s_eo, s_eoo, stream)
+        for _ in range(8):
+            codec.decode_into(s_h, s_hoff, n, s_do, s_doo, s_st, stream)
+        torch.cuda.synchronize()
+        codec.timing(True)
+        codec.encode_into(d, o, n, 0, eo, eoo, stream)
+        torch.cuda.synchronize()
+        first_e = [u for k, u in codec.timing_read() if k == qhuff.KIND_ENCODE]
+        var_e = codec.kernel_variant(qhuff.KIND_ENCODE)
+        codec.timing(False)
+        for _ in range(8):
+            codec.decode_into(s_h, s_hoff, n, s_do, s_doo, s_st, stream)
+        torch.cuda.synchronize()
+        codec.timing(True)
+        codec.decode_into(h, eoo, n, do, doo, st, stream)
+        torch.cuda.synchronize()
+        first_d = [u for k, u in codec.timing_read() if k == qhuff.KIND_DECODE]
+        var_d = codec.kernel_variant(qhuff.KIND_DECODE)
+        codec.timing(False)
+        first_ok = (torch.equal(do[:raw], d) and not bool(st.any()))
+        for _ in range(2):
             codec.encode_into(d, o, n, 0, eo, eoo, stream)
             codec.decode_into(h, eoo, n, do, doo, st, stream)
-            torch.cuda.synchronize()
+        torch.cuda.synchronize()
         codec.timing(True)
         for _ in range(K):
             codec.encode_into(d, o, n, 0, eo, eoo, stream)
@@ -636,10 +667,17 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
                "dec_payload_gbps": round(raw / (d_us * 1e-6) / 1e9, 1),
                "enc_dec_gbps": round(gbps, 1),
                "vs_synthetic_token": round(gbps / syn_gbps, 3),
+               "first_launch_us": {"enc": round(first_e[0], 2),
+                                   "dec": round(first_d[0], 2),
+                                   "enc_vs_mean": round(first_e[0] / e_us, 3),
+                                   "dec_vs_mean": round(first_d[0] / d_us, 3),
+                                   "full_loop": [var_e, var_d],
+                                   "roundtrip_ok": bool(first_ok)},
                "roundtrip_ok": bool(ok)}
         ent.update(W.tile_shares(data, off, hoff))
         out[name] = ent
         del d, o, eo, eoo, h, do, doo, st
+    del s_eo, s_eoo, s_do, s_doo, s_st
     return out
 
 

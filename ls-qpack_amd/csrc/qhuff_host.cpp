@@ -152,8 +152,12 @@ struct qhuff_ctx
     uint32_t *err;                       // device: [0] error word, [1..3]
                                          // census, then claim counters
     uint64_t cap_tiles, cap_super;
-    uint8_t *big;                        // device: big-tile output slots
-                                         // (Coord::big), kBigSlots per wave
+    uint8_t *big_small;                  // device: big-tile output slots
+                                         // (Coord::big) of launches of at
+                                         // most kSmallGrid workgroups, lazily;
+                                         // larger launches use the device's
+                                         // pool (slot_pool)
+    bool pool_ref;                       // holds a reference on that pool
     // kernel variant per kind (0 encode, 1 decode): the lean kernel by
     // default; the full one (big-tile slots, cooperative long strings) once
     // a launch reports such tiles, until kCalm launches in a row have none
@@ -231,6 +235,142 @@ fail(qhuff_ctx *c, hipError_t e, const char *what)
             return fail((c), e_, #call);                                     \
     } while (0)
 
+// ---- big-tile output slots ---------------------------------------------------
+//
+// A launch in auto or full-only mode may code big tiles through kBigSlots
+// global slots per wave of its grid (qhuff_pipeline.h tile_loop): 48 KB a
+// wave, 151 MB for the resident grid of 256 CUs.  A launch of at most
+// kSmallGrid workgroups (the per-string entry points, small batches) uses a
+// region of its own context, allocated at its first such launch (4.7 MB);
+// larger ones share one pool per device, allocated at the first such launch
+// of any context and freed with the last context that used it.  So a
+// context's own device memory stays small (tables, look-back flags, its
+// staging), however many contexts a process opens.  Contexts order their
+// launches on the pool: while more than one context holds it, each launch
+// on it records the pool's event, and a launch of another context waits for
+// it first (a context's own launches are ordered by prepare_launch); a
+// context that joins a pool in use waits for the device once.
+constexpr uint32_t kSmallGrid = 8;
+constexpr uint64_t kWaveSlotBytes = (uint64_t) kBigSlots * kBigSlotBytes;
+constexpr int kMaxDevices = 64;
+
+struct SlotPool
+{
+    std::mutex mu;
+    uint8_t *p = nullptr;
+    uint64_t waves = 0;                  // slots for this many waves
+    int refs = 0;                        // contexts that used it
+    hipEvent_t ev = nullptr;             // the last launch on it (refs > 1)
+    const qhuff_ctx *ev_ctx = nullptr;   // whose launch ev follows
+};
+static SlotPool g_pool[kMaxDevices];
+
+static void
+pool_release(int device)
+{
+    if (device < 0 || device >= kMaxDevices)
+        return;
+    SlotPool &sp = g_pool[device];
+    std::lock_guard<std::mutex> g(sp.mu);
+    if (--sp.refs > 0)
+        return;
+    if (sp.p)
+        (void) hipFree(sp.p);
+    if (sp.ev)
+        (void) hipEventDestroy(sp.ev);
+    sp.p = nullptr;
+    sp.waves = 0;
+    sp.ev = nullptr;
+    sp.ev_ctx = nullptr;
+}
+
+static uint64_t
+max_grid_waves(const qhuff_ctx *c)
+{
+    const uint64_t e = (uint64_t) c->enc_grid * encode_waves_per_block();
+    const uint64_t d = (uint64_t) c->dec_grid * decode_waves_per_block();
+    return e > d ? e : d;
+}
+
+// Runs launch(slots) for a launch of `grid` workgroups of `wpb` waves: the
+// big-tile slots a full kernel needs (*full), null for the lean one.  When
+// they cannot be allocated the launch runs the lean kernel (*full is
+// cleared): big tiles out of line, the same output.
+template <class F>
+static int
+with_slots(qhuff_ctx *c, uint32_t grid, uint64_t wpb, bool *full,
+           hipStream_t st, F launch)
+{
+    if (!*full)
+        return launch((uint8_t *) nullptr);
+    if (grid <= kSmallGrid)
+    {
+        if (!c->big_small)
+        {
+            const uint64_t w = (uint64_t) kSmallGrid
+                * (uint64_t) (encode_waves_per_block() > decode_waves_per_block()
+                              ? encode_waves_per_block() : decode_waves_per_block());
+            if (hipMalloc((void **) &c->big_small, w * kWaveSlotBytes) != hipSuccess)
+            {
+                c->big_small = nullptr;
+                (void) hipGetLastError();
+                *full = false;
+                return launch((uint8_t *) nullptr);
+            }
+        }
+        return launch(c->big_small);
+    }
+    if (c->device < 0 || c->device >= kMaxDevices)
+    {
+        *full = false;
+        return launch((uint8_t *) nullptr);
+    }
+    SlotPool &sp = g_pool[c->device];
+    std::lock_guard<std::mutex> g(sp.mu);
+    if (!c->pool_ref)
+    {
+        // joining: another context's launches on the pool are not recorded
+        // while it was alone -- wait for them once
+        if (sp.refs > 0)
+            HIPCHK(c, hipDeviceSynchronize());
+        ++sp.refs;
+        c->pool_ref = true;
+    }
+    const uint64_t need = (uint64_t) grid * wpb;
+    if (sp.waves < need)
+    {
+        if (sp.p)
+        {
+            // (a grid larger than any seen: every user idle first)
+            HIPCHK(c, hipDeviceSynchronize());
+            (void) hipFree(sp.p);
+            sp.p = nullptr;
+            sp.waves = 0;
+        }
+        const uint64_t mw = max_grid_waves(c);
+        const uint64_t w = mw > need ? mw : need;
+        if (hipMalloc((void **) &sp.p, w * kWaveSlotBytes) != hipSuccess)
+        {
+            sp.p = nullptr;
+            (void) hipGetLastError();
+            *full = false;
+            return launch((uint8_t *) nullptr);
+        }
+        sp.waves = w;
+    }
+    if (sp.ev && sp.ev_ctx && sp.ev_ctx != c)
+        HIPCHK(c, hipStreamWaitEvent(st, sp.ev, 0));
+    const int rc = launch(sp.p);
+    if (rc == QHUFF_OK && sp.refs > 1)
+    {
+        if (!sp.ev)
+            HIPCHK(c, hipEventCreateWithFlags(&sp.ev, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(sp.ev, st));
+        sp.ev_ctx = c;
+    }
+    return rc;
+}
+
 extern "C" int
 qhuff_open(int device, qhuff_ctx **ctx_out)
 {
@@ -295,15 +435,6 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         e = hipMalloc((void **) &c->err, kErrWords * sizeof(uint32_t));
     if (e == hipSuccess)
         e = hipMemset(c->err, 0, kErrWords * sizeof(uint32_t));
-    if (e == hipSuccess)
-    {
-        // kBigSlots output slots per wave of the larger grid (192 MB on
-        // 256 CUs): big tiles (qhuff_pipeline.h)
-        const uint64_t waves = (uint64_t) (c->enc_grid > c->dec_grid
-                                           ? c->enc_grid : c->dec_grid)
-                             * kBigMaxWaves;
-        e = hipMalloc((void **) &c->big, waves * kBigSlots * kBigSlotBytes);
-    }
     if (e == hipSuccess)
         e = hipHostMalloc((void **) &c->rare_host, 4 * sizeof(uint32_t),
                           hipHostMallocMapped | hipHostMallocCoherent);
@@ -376,8 +507,10 @@ qhuff_close(qhuff_ctx *c)
         (void) hipFree(c->tab);
     if (c->flags)
         (void) hipFree(c->flags);
-    if (c->big)
-        (void) hipFree(c->big);
+    if (c->big_small)
+        (void) hipFree(c->big_small);
+    if (c->pool_ref)
+        pool_release(c->device);
     if (c->rare_host)
         (void) hipHostFree(c->rare_host);
     if (c->err)
@@ -566,28 +699,39 @@ coord(qhuff_ctx *c, uint64_t tiles)
     k.epoch = c->epoch;
     k.n_tiles = (uint32_t) tiles;
     k.spread = 0;
-    k.big = c->big;
+    k.big = nullptr;                     // (with_slots)
     k.rare = nullptr;
     return k;
 }
 
-// the event pair of the next launch (kind QHUFF_KIND_*) with timing on:
-// *e0 = *e1 = null otherwise
-static void
+// the event pair of the next launch (kind QHUFF_KIND_*) with timing on, and
+// its ring slot; *e0 = *e1 = null and kNoTiming otherwise.  The slot is
+// taken by timing_commit once the launch has gone out: a launch that fails
+// leaves no slot with unrecorded events behind.
+constexpr uint32_t kNoTiming = 0xffffffffu;
+static uint32_t
 timing_slot(qhuff_ctx *c, uint32_t kind, hipEvent_t *e0, hipEvent_t *e1)
 {
     *e0 = *e1 = nullptr;
     if (!c->t_on)
-        return;
+        return kNoTiming;
     // sampled: each timed launch costs the step ~4.6 us of queue time
     // (tools/timing_cost.py: 114.8 vs 105.6 us per encode + decode step)
     if (c->t_seen[kind]++ % c->t_every != 0)
-        return;
+        return kNoTiming;
     const uint32_t k = (uint32_t) (c->t_next % QHUFF_TIMING_SLOTS);
-    c->t_kind[k] = (uint8_t) kind;
-    ++c->t_next;
     *e0 = c->tev[2 * k];
     *e1 = c->tev[2 * k + 1];
+    return k;
+}
+
+static void
+timing_commit(qhuff_ctx *c, uint32_t k, uint32_t kind)
+{
+    if (k == kNoTiming)
+        return;
+    c->t_kind[k] = (uint8_t) kind;
+    ++c->t_next;
 }
 
 extern "C" int
@@ -683,7 +827,10 @@ grid_for(const qhuff_ctx *c, uint64_t tiles, uint64_t waves_per_block,
 // launches seen to have run -- not issued: a burst of launches is issued
 // long before the first of them reports.  (The lean kernel codes those
 // tiles correctly but slowly; the full one carries their code beside the
-// tile loop, which costs the loop ~5 % on batches that never need it.)
+// tile loop, which costs the loop ~5 % on batches that never need it.
+// Choosing inside the launch instead -- each wave lean until its first
+// such tile, then full -- was built three ways in round 5 and measured
+// slower: DESIGN.md section 6.)
 static constexpr uint32_t kCalm = 8;
 static bool
 pick_full(qhuff_ctx *c, int kind, Coord *k)
@@ -751,10 +898,18 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.c = coord(c, tiles);
     const uint64_t wpb = (uint64_t) encode_waves_per_block();
     const uint32_t grid = grid_for(c, tiles, wpb, c->enc_grid, &a.c.spread);
-    hipEvent_t e0, e1;
-    timing_slot(c, QHUFF_KIND_ENCODE, &e0, &e1);
-    const bool full = pick_full(c, 0, &a.c);
-    HIPCHK(c, launch_encode(a, grid, st, e0, e1, full));
+    bool full = pick_full(c, 0, &a.c);
+    rc = with_slots(c, grid, wpb, &full, st, [&](uint8_t *slots) -> int {
+        a.c.big = slots;
+        hipEvent_t e0, e1;
+        const uint32_t ts = timing_slot(c, QHUFF_KIND_ENCODE, &e0, &e1);
+        HIPCHK(c, launch_encode(a, grid, st, e0, e1, full));
+        timing_commit(c, ts, QHUFF_KIND_ENCODE);
+        return QHUFF_OK;
+    });
+    if (rc)
+        return rc;
+    c->last_full[0] = full;
     return finish_launch(c, st);
 }
 
@@ -790,10 +945,24 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.lp = c->lp;
     const uint64_t wpb = (uint64_t) decode_waves_per_block();
     const uint32_t grid = grid_for(c, tiles, wpb, c->dec_grid, &a.c.spread);
-    hipEvent_t e0, e1;
-    timing_slot(c, QHUFF_KIND_DECODE, &e0, &e1);
-    const bool full = pick_full(c, 1, &a.c);
-    HIPCHK(c, launch_decode(a, grid, st, e0, e1, c->keep_rejected, full));
+    // (keep: the per-string replay -- the lean keep kernel, never timed, and
+    // outside the variant choice of the batch kernel: ADVICE r04)
+    bool full = false;
+    if (!c->keep_rejected)
+        full = pick_full(c, 1, &a.c);
+    rc = with_slots(c, grid, wpb, &full, st, [&](uint8_t *slots) -> int {
+        a.c.big = slots;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        const uint32_t ts = c->keep_rejected
+            ? kNoTiming : timing_slot(c, QHUFF_KIND_DECODE, &e0, &e1);
+        HIPCHK(c, launch_decode(a, grid, st, e0, e1, c->keep_rejected, full));
+        timing_commit(c, ts, QHUFF_KIND_DECODE);
+        return QHUFF_OK;
+    });
+    if (rc)
+        return rc;
+    if (!c->keep_rejected)
+        c->last_full[1] = full;
     return finish_launch(c, st);
 }
 
@@ -819,8 +988,9 @@ hash_call(qhuff_ctx *c, const uint8_t *in, const uint32_t *off, uint32_t n,
     a.seed = seed;
     a.pairs = pairs ? 1u : 0u;
     hipEvent_t e0, e1;
-    timing_slot(c, QHUFF_KIND_HASH, &e0, &e1);
+    const uint32_t ts = timing_slot(c, QHUFF_KIND_HASH, &e0, &e1);
     HIPCHK(c, launch_hash(a, c->hash_grid, (hipStream_t) stream, e0, e1));
+    timing_commit(c, ts, QHUFF_KIND_HASH);
     return QHUFF_OK;
 }
 

@@ -373,11 +373,14 @@ def test_decode_cooperative_invalid(codec):
 
 @pytest.mark.parametrize("kernels", ["lean", "full", "auto"])
 def test_kernel_variants(kernels):
-    """Each kernel of a kind is exact on its own (qhuff_host.cpp pick_full):
-    the lean one, which codes big tiles and long strings on the round-3 path,
-    the full one (big-tile slots, cooperative long strings), and the switch
-    between them -- auto starts lean, and its later launches of the same
-    batches run full once the rare flag is set; each case is run twice."""
+    """Each kernel of a kind is exact on its own (qhuff_host.cpp pick_full,
+    QHUFF_KERNELS): the lean one, which codes big tiles and long strings on
+    the round-3 path, the full one (big-tile slots, cooperative long
+    strings), and the switch between them -- auto starts lean, and its later
+    launches of the same batches run full once the rare flag is set -- on
+    big tiles, multi-unit tiles, a tile whose output exceeds a slot (the
+    70 KB string among short ones: parked pending tiles, then the slow
+    tile) and cooperative strings; each case twice."""
     import qhuff
     old = os.environ.get("QHUFF_KERNELS")
     os.environ["QHUFF_KERNELS"] = kernels
@@ -389,10 +392,21 @@ def test_kernel_variants(kernels):
         else:
             os.environ["QHUFF_KERNELS"] = old
     try:
+        rng = random.Random(9)
+        huge = bytes(rng.choice(ALPHAS["all"]) for _ in range(70000))
+        mixed = pack(rand_strings(rng, 300, ALPHAS["token"], 0, 40) + [huge]
+                     + rand_strings(rng, 300, ALPHAS["token"], 0, 40))
         for _ in range(2):
             test_big_tile_slots(c)
+            test_multi_unit_tiles(c, 100, 400)
             test_decode_cooperative_long_strings(c, "token")
             test_decode_cooperative_invalid(c)
+            for mode in (0, 7):
+                check_encode(c, *mixed, mode)
+            h, ho = O.encode_batch(*mixed, 0)
+            out, oo, st = check_decode(c, h, ho)
+            assert np.array_equal(out, mixed[0])
+        assert c.device_error() == 0
     finally:
         c.close()
 
@@ -488,6 +502,20 @@ def test_launch_timing(codec):
     assert all(u > 0 for _, u in t)
     check_encode(codec, data, off, 0)
     assert codec.timing_read() == []
+    # the per-string entry point on an invalid string: its decode launch is
+    # timed, the replay that follows (a decode launch of the keep kernel) is
+    # not and leaves the ring alone (it took a slot whose events
+    # it never recorded)
+    codec.timing(True)
+    check_encode(codec, data, off, 0)
+    r = codec.huff_decode(b"\xff\xff\xff\xff", 64)
+    assert r[0] == qhuff.HUFF_DEC_ERROR
+    check_decode(codec, h, ho)
+    t = codec.timing_read()
+    codec.timing(False)
+    E, D = qhuff.KIND_ENCODE, qhuff.KIND_DECODE
+    assert [k for k, _ in t] == [E, D, D]
+    assert all(u > 0 for _, u in t)
 
 
 def _launch_shape_check(c, n, seed):
