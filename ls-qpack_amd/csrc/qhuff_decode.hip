@@ -63,6 +63,8 @@ qhuff_decode_kernel(DecArgs a)
     }
     const QH_GLB uint16_t *gs = glb(a.sorted);
     const uint16_t so = gs[tid < 257 ? tid : 0];
+    static_assert(kLong2Size <= 64 * kWaves, "one long2 entry per thread");
+    const uint16_t l2 = glb(a.long2)[tid < kLong2Size ? tid : 0];
     claim_block_store(a.c, cb, &sm->tk, QH_DEC_PER);
     clear_next_launch(a.c);
     // the tickets: LDS stores visible, no wait for the table loads (a
@@ -87,6 +89,8 @@ qhuff_decode_kernel(DecArgs a)
         }
         if (tid < 257)
             sm->sorted[tid] = so;
+        if (tid < kLong2Size)
+            sm->long2[tid] = l2;
         if (tid == 0)
             sm->win[kHoldIdx] = kHoldEntry;
         __syncthreads();             // the tables

@@ -70,6 +70,7 @@ struct DecSmem
 {
     uint32_t win[kWinSize + 4];      // + the hold entry
     uint16_t sorted[257];
+    uint16_t long2[kLong2Size];      // long codes by leading ones
     DecWave w[kWaves];
     BlockTickets tk;                 // the workgroup's first tickets
 };
@@ -281,7 +282,7 @@ template <class Emit, bool R2 = true>
 __device__ __forceinline__ int
 decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
                   const QH_LDS uint32_t *s_win, const QH_LDS uint16_t *s_sorted,
-                  Emit &emit)
+                  const QH_LDS uint16_t *s_long2, Emit &emit)
 {
     uint32_t rem = bitend - bit0;            // real bits not yet consumed
     uint32_t A, B, t, p, nx;
@@ -311,11 +312,15 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
              | (live ? 0u : 4u * kHoldIdx);
     };
     uint32_t idx = win_addr(W, rem >= kMain);
-    // A long-code marker entry (e < 2^24: c = ns = 0) stalls its lane where
-    // it is, like the hold entry.  The step loop runs while some lane with
-    // >= kMain bits left is not stalled -- so the step carries no long-code
-    // branch -- and the stalled lanes then take their long step together,
-    // outside the loop, and the loop resumes.
+    // A long-code marker entry (e < 2^24: c = ns = 0, no bytes) stalls its
+    // lane where it is, like the hold entry, for the rest of the loop trip;
+    // at the trip's end, if any lane is stalled, the stalled lanes take
+    // their long step at once (one count of leading ones, one long2 lookup),
+    // the others wait that one step.  (Until round 4 the stalled lanes
+    // waited until every live lane was stalled or done: on text with ~2 %
+    // long-code bytes a wave then ran its step count about twice,
+    // alphabet C decoded at 1.9x the token batch's time.)  The token
+    // batch's step is unchanged: one more scalar test per trip.
     auto advance = [&](uint32_t c) {
         uint32_t tn;
         const bool cross = __builtin_sub_overflow(t, c, &tn);
@@ -324,57 +329,59 @@ decode_string_lds(const QH_LDS uint32_t *src, uint32_t bit0, uint32_t bitend,
         t = tn & 31;
         p += cross ? 1u : 0u;
     };
-    for (;;)
+    if (__builtin_amdgcn_ballot_w64(rem >= kMain))
+    do
     {
-        uint32_t e = kHoldEntry;
-        if (__builtin_amdgcn_ballot_w64(rem >= kMain))
-        do
-        {
-            e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
-            const uint32_t c = ent_c(e);
-            emit(e, ent_ns(e));
-            rem -= c;
-            advance(c);
-            if constexpr (!R2)
-                nx = src[p];
-            W = __builtin_amdgcn_alignbit(A, B, t);
-            idx = win_addr(W, rem >= kMain);
-            if constexpr (R2)
-            {
-                // A second step on the same refill: a main step consumes at
-                // most 13 bits, and a step that moves the window on a dword
-                // leaves t >= 19, so the two steps cross at most one dword
-                // boundary and the next dword nx read before them covers it.
-                // (A lane that stalled or went on hold in the first step
-                // reads the same entry again and consumes nothing.)
-                e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
-                const uint32_t c2 = ent_c(e);
-                emit(e, ent_ns(e));
-                rem -= c2;
-                advance(c2);
-                nx = src[p];
-                W = __builtin_amdgcn_alignbit(A, B, t);
-                idx = win_addr(W, rem >= kMain);
-            }
-        } while (__builtin_amdgcn_ballot_w64((rem >= kMain) & (e >= (1u << 24))));
-        // lanes left with >= kMain bits sit on a code of 14..30 bits; EOS,
-        // or a code running past the end, rejects the string (D3)
-        if (__builtin_expect(!__builtin_amdgcn_ballot_w64(rem >= kMain), 1))
-            break;
-        const bool lng = rem >= kMain;
-        uint32_t L;
-        const uint32_t sym = long_code(W, s_sorted, &L);
-        const bool rej = lng & ((sym == 256) | (L > rem));
-        const bool ok = lng & !rej;
-        const uint32_t c = ok ? L : 0u;
-        emit(sym, ok ? 1u : 0u);
-        bad |= rej ? 1u : 0u;
-        rem = rej ? 0u : rem - c;
+        uint32_t e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
+        const uint32_t c = ent_c(e);
+        emit(e, ent_ns(e));
+        rem -= c;
         advance(c);
-        nx = src[p];
+        if constexpr (!R2)
+            nx = src[p];
         W = __builtin_amdgcn_alignbit(A, B, t);
         idx = win_addr(W, rem >= kMain);
-    }
+        if constexpr (R2)
+        {
+            // A second step on the same refill: a main step consumes at
+            // most 13 bits, and a step that moves the window on a dword
+            // leaves t >= 19, so the two steps cross at most one dword
+            // boundary and the next dword nx read before them covers it.
+            // (A lane that stalled or went on hold in the first step
+            // reads the same entry again and consumes nothing.)
+            e = *(const QH_LDS uint32_t *) ((const QH_LDS uint8_t *) s_win + idx);
+            const uint32_t c2 = ent_c(e);
+            emit(e, ent_ns(e));
+            rem -= c2;
+            advance(c2);
+            nx = src[p];
+            W = __builtin_amdgcn_alignbit(A, B, t);
+            idx = win_addr(W, rem >= kMain);
+        }
+        // lanes with >= kMain bits on a marker sit on a code of 14..30
+        // bits; EOS, or a code running past the end, rejects the string (D3)
+        const bool lng = (rem >= kMain) & (e < (1u << 24));
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(lng) != 0, 0))
+        {
+            // (a long step consumes at most 30 bits: it crosses at most one
+            // dword, which nx holds)
+            const uint32_t n1 = min(~W ? (uint32_t) __builtin_clz(~W) : 32u,
+                                    31u);
+            const uint32_t x = (W << ((n1 + 1) & 31)) >> 27;
+            const uint32_t l2 = s_long2[(lng ? n1 - kLong2N1 : 0u) * 32 + x];
+            const uint32_t sym = l2 & 511, L = (l2 >> 9) + 14;
+            const bool rej = lng & ((sym == 256) | (L > rem));
+            const bool ok = lng & !rej;
+            const uint32_t cl = ok ? L : 0u;
+            emit(sym, ok ? 1u : 0u);
+            bad |= rej ? 1u : 0u;
+            rem = rej ? 0u : rem - cl;
+            advance(cl);
+            nx = src[p];
+            W = __builtin_amdgcn_alignbit(A, B, t);
+            idx = win_addr(W, rem >= kMain);
+        }
+    } while (__builtin_amdgcn_ballot_w64(rem >= kMain));
 
     // epilogue, one pass: the last < kWinBits (13) real bits hold at most
     // two symbols (codes are >= 5 bits), both inside the window padded with
@@ -1066,7 +1073,7 @@ struct DecPolicyT
         {
             ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
             r = decode_string_lds(wv->in, 8 * rs, mine ? 8 * rs : 8 * re,
-                                  sm->win, sm->sorted, em);
+                                  sm->win, sm->sorted, sm->long2, em);
         }
         *sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
         *st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
@@ -1119,7 +1126,7 @@ struct DecPolicyT
             ArenaEmit em{d0, d0, 0};
             const int r2 = decode_string_lds(wv->in, 8 * rs,
                                              f ? 8 * re : 8 * rs, sm->win,
-                                             sm->sorted, em);
+                                             sm->sorted, sm->long2, em);
             r = f ? r2 : r;
         }
         if (mine)

@@ -30,6 +30,7 @@ struct DevTables
     uint32_t win[kWinSize];              // 16-byte aligned (copied as uint4)
     uint2 enc[257];                      // {code, bits}
     uint16_t sorted[257];
+    uint16_t long2[kLong2Size];
 };
 
 // Host copy workers for the PCIe-inclusive path: a staging memcpy of tens
@@ -398,6 +399,7 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         dt.enc[i] = make_uint2(ht->code[i], ht->bits[i]);
     memcpy(dt.win, ht->win, sizeof(dt.win));
     memcpy(dt.sorted, ht->sorted, sizeof(dt.sorted));
+    memcpy(dt.long2, ht->long2, sizeof(dt.long2));
     memset(&c->lp, 0, sizeof(c->lp));
     c->lp.n = ht->n_long;
     memcpy(c->lp.l, ht->longc, sizeof(LongLen) * ht->n_long);
@@ -940,6 +942,7 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.status = status;
     a.win = c->tab->win;
     a.sorted = c->tab->sorted;
+    a.long2 = c->tab->long2;
     a.n = n;
     a.c = coord(c, tiles);
     a.lp = c->lp;
@@ -1345,6 +1348,7 @@ svc_ensure_running(qhuff_svc *v)
     a.active = v->active;
     a.win = c->tab->win;
     a.sorted = c->tab->sorted;
+    a.long2 = c->tab->long2;
     a.enc = c->tab->enc;
     a.idle_ticks = v->idle_ticks;
     a.life_ticks = v->life_ticks;

@@ -38,6 +38,7 @@ struct DecArgs
     uint8_t *status;
     const uint32_t *win;         // kWinSize window entries
     const uint16_t *sorted;      // 257 symbols in canonical order
+    const uint16_t *long2;       // kLong2Size long codes by leading ones
     uint64_t n;
     Coord c;
     LongParams lp;
@@ -121,6 +122,7 @@ struct SvcArgs
     uint64_t *active;            // device: last time any wave served (100 MHz)
     const uint32_t *win;
     const uint16_t *sorted;
+    const uint16_t *long2;
     const uint2 *enc;
     uint64_t idle_ticks;         // a wave leaves after this long with no
                                  // request served by any wave (100 MHz ticks)

@@ -41,6 +41,7 @@ struct SvcSmem
     static constexpr bool kMtRep = false;   // (no LDS left for 32 copies)
     uint32_t win[kWinSize + 4];      // decode window table + the hold entry
     uint16_t sorted[257];
+    uint16_t long2[kLong2Size];      // decode: long codes by leading ones
     u32x2 enc[257];                  // encode tables (enc_tables_load)
     uint32_t mt[256];
     uint8_t len[256];
@@ -176,6 +177,8 @@ qhuff_service_kernel(SvcArgs a)
             sw[i] = gw[i];
         if (tid < 257)
             sm->sorted[tid] = glb(a.sorted)[tid];
+        for (int i = tid; i < kLong2Size; i += 64 * kWaves)
+            sm->long2[i] = glb(a.long2)[i];
         if (tid == 0)
             sm->win[kHoldIdx] = kHoldEntry;          // (decode)
         enc_tables_load(sm, a.enc, tid);

@@ -90,6 +90,23 @@ build_tables(HostTables *t)
         t->win[w] = e;
     }
 
+    for (int r = 0; r < kLong2Rows; ++r)
+        for (uint32_t x = 0; x < 32; ++x)
+        {
+            const int n1 = kLong2N1 + r;
+            // n1 ones, a zero, then x's 5 bits (fewer when they run out)
+            uint32_t w = n1 >= 32 ? 0xffffffffu : ~(0xffffffffu >> n1);
+            if (n1 <= 26)
+                w |= x << (26 - n1);
+            else if (n1 < 31)
+                w |= x >> (n1 - 26);
+            int L;
+            const int sym = canon_decode(&c, w, 30, &L);
+            t->long2[r * 32 + x] = sym >= 0 && L > kWinBits
+                ? (uint16_t) ((uint32_t) sym | ((uint32_t) (L - 14) << 9))
+                : (uint16_t) 0xffff;
+        }
+
     t->n_long = 0;
     for (int L = kWinBits + 1; L <= 30; ++L)
         if (c.count[L])

@@ -15,6 +15,7 @@
 //                 decoder step for long codes (the reference switches to its
 //                 nibble FSM there, lsqpack.c:5452-5465)
 //   sorted[257]   symbols in canonical order (index -> symbol)
+//   long2[640]    long codes by leading ones + 5 bits (decoder long step)
 #pragma once
 #include <stdint.h>
 
@@ -80,6 +81,16 @@ make_long_tab()
 
 constexpr LongTab kLongTab = make_long_tab();
 
+// Long codes (14..30 bits) by their leading ones: every such code starts
+// with n1 >= 12 ones, and after its first zero has at most 5 more bits
+// (RFC 7541 Appendix B).  long2[(min(n1, 31) - 12) * 32 + the 5 bits after
+// the first zero] = sym | (L - 14) << 9 (0xffff: no code of 14..30 bits
+// there); n1 >= 30 is the EOS code (sym 256, L 30).  The decoder's in-loop
+// long step: a count of leading ones and one lookup.
+constexpr int kLong2N1 = 12;
+constexpr int kLong2Rows = 32 - kLong2N1;
+constexpr int kLong2Size = kLong2Rows * 32;
+
 struct HostTables
 {
     uint32_t code[257];
@@ -88,6 +99,7 @@ struct HostTables
     LongLen longc[kMaxLong];
     uint32_t n_long;
     uint16_t sorted[257];
+    uint16_t long2[kLong2Size];
 };
 
 void build_tables(HostTables *t);

@@ -77,7 +77,7 @@ struct AddtidEmit
     __device__ __forceinline__ void finish() {}
     __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
     {
-        const uint32_t m0 = base + ((step & 15u) << 8);
+        const uint32_t m0 = __builtin_amdgcn_readfirstlane(base + ((step & 15u) << 8));
         asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tds_write_addtid_b32 %0"
                      : : "v"(val), "s"(m0) : "m0", "memory");
         ++step;
@@ -127,30 +127,30 @@ lab(DecArgs a, int reps, MbOut *res)
         if (MODE == 0)
         {
             ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
-            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
         }
         else if (MODE == 1)
         {
             NullEmit em{0, 0};
-            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
         }
         else if (MODE == 2)
         {
             // lane-major records: lane l's at arena + 76 * l (76 B = 19
             // dwords, odd: the 32 lanes of a group on distinct banks)
             RecEmit em{(QH_LDS uint16_t *) (wv->arena + 76 * lane), 0};
-            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
         }
         else if (MODE == 3)
         {
             OneByteEmit em{wv->arena + slot0, wv->arena + slot0, 0};
-            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
         }
         else if (MODE == 7 || MODE == 8)
         {
             const uint32_t sl = MODE == 7 ? slot0 : 84 * lane;
             U16Emit em{wv->arena + sl, wv->arena + sl, 0};
-            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
         }
         else if (MODE == 9 || MODE == 10)
         {
@@ -158,8 +158,8 @@ lab(DecArgs a, int reps, MbOut *res)
             // (9) or per two steps (10, QH_REFILL2)
             ArenaEmit em{wv->arena + 108 * lane, wv->arena + 108 * lane, 0};
             n = MODE == 9
-                ? decode_string_lds<ArenaEmit, false>(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em)
-                : decode_string_lds<ArenaEmit, true>(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+                ? decode_string_lds<ArenaEmit, false>(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em)
+                : decode_string_lds<ArenaEmit, true>(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
         }
         else
         {
@@ -168,7 +168,7 @@ lab(DecArgs a, int reps, MbOut *res)
             // lanes at equal progress on distinct banks)
             constexpr uint32_t STRIDE = MODE == 4 ? 84 : MODE == 5 ? 76 : 68;
             ArenaEmit em{wv->arena + STRIDE * lane, wv->arena + STRIDE * lane, 0};
-            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
         }
         sum += read_lane((uint32_t) n, 63);
         const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -194,6 +194,7 @@ struct AddtidSmem
     uint32_t arena[W][1024];                 // 16 steps x 64 lanes x 4 B
     uint32_t win[kWinSize + 4];
     uint16_t sorted[257];
+    uint16_t long2[kLong2Size];   // (not loaded: the lab strings have no long codes)
     alignas(16) uint32_t in[W][kDecStageCap / 4];
 };
 
@@ -230,7 +231,7 @@ lab_addtid(DecArgs a, int reps, MbOut *res)
         const uint64_t t0 = __builtin_amdgcn_s_memtime();
         AddtidEmit em{(uint32_t) __builtin_amdgcn_readfirstlane((int) base), 0, 0};
         int n = decode_string_lds(sm->in[w], 8 * rs, 8 * re, sm->win,
-                                  sm->sorted, em);
+                                  sm->sorted, sm->long2, em);
         sum += read_lane((uint32_t) n, 63);
         const uint64_t t1 = __builtin_amdgcn_s_memtime();
         c0 += t1 - t0;
