@@ -5,9 +5,11 @@
 # of in-process A/Bs (tools/ab_inproc.py), each pair in both orders, each in
 # a fresh process (the first library's context of a process has shown a
 # 2-4 % bias, which the pairs cancel).  Optional third argument: also the
-# step lab's refill A/B.  Usage: TAG CAND [lab]
+# step lab's refill A/B.  WORKLOADS="corpus alphabet_c": one more pair per
+# real-workload batch (qhuff/workload.py), printed after the summary.
+# Usage: TAG CAND [lab]
 set -e
-cd "$GRAFT_REPO_ROOT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 o=gpurun_out/$1
 b=${BASE:-libqhuff_base.so}
 mkdir -p $o
@@ -21,6 +23,10 @@ fi
 for r in $(seq 1 ${REPS:-3}); do
   timeout -k 10 300 python -u tools/ab_inproc.py ls-qpack_amd/$2 ls-qpack_amd/$b 20 10 > $o/ab_${r}_cb.json
   timeout -k 10 300 python -u tools/ab_inproc.py ls-qpack_amd/$b ls-qpack_amd/$2 20 10 > $o/ab_${r}_bc.json
+done
+for w in $WORKLOADS; do
+  WORKLOAD=$w timeout -k 10 300 python -u tools/ab_inproc.py ls-qpack_amd/$2 ls-qpack_amd/$b 6 5 > $o/wl_${w}_cb.json
+  WORKLOAD=$w timeout -k 10 300 python -u tools/ab_inproc.py ls-qpack_amd/$b ls-qpack_amd/$2 6 5 > $o/wl_${w}_bc.json
 done
 python - $o <<'PY'
 import glob, json, statistics, sys
@@ -41,3 +47,14 @@ for k in ("enc", "dec"):
              statistics.mean(rat[k]), " ".join("%.3f" % r for r in rat[k])))
 json.dump({"cand": cand, "base": base, "ratio": rat}, open(o + "/ab_summary.json", "w"))
 PY
+for w in $WORKLOADS; do
+  python - $o/wl_${w}_cb.json $o/wl_${w}_bc.json <<'PY'
+import json, sys
+a, b = (json.load(open(f)) for f in sys.argv[1:3])
+for k in ("enc", "dec"):
+    c = (a["a_%s_med" % k] + b["b_%s_med" % k]) / 2
+    s = (a["b_%s_med" % k] + b["a_%s_med" % k]) / 2
+    print("%s %s: candidate %.2f us, base %.2f us, cand/base %.4f"
+          % (a["workload"], k, c, s, c / s))
+PY
+done

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Round-end evidence on one GPU box.  Every GPU step has its own time limit;
 # a step that crashes or times out ends the session (a failing test does
-# not stop the measurements).  Usage: tools/r04_final.sh TAG
+# not stop the measurements).  Usage: tools/round_evidence.sh TAG
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-tag=${1:-r04_final}
+tag=${1:-round_final}
 o=gpurun_out/$tag
 mkdir -p $o
 fatal() { [ "$1" -ge 124 ] && { echo "step rc=$1: stopping"; exit "$1"; }; return 0; }
