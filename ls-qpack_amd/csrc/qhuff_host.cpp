@@ -169,6 +169,9 @@ struct qhuff_ctx
     uint32_t calm[2];
     uint32_t seen[2];                    // rare_host[2 kind + 1] last read
     bool last_full[2];                   // variant of the last launch
+    int hint[2];                         // the next launch's variant from
+                                         // its batch, known on the host
+                                         // (host_hint), or -1: history
     int kernels;                         // QHUFF_KERNELS: 0 auto, 1 lean,
                                          // 2 full
     unsigned long long *prof;            // QHUFF_PROFILE builds: stamp buffer
@@ -466,6 +469,7 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
         return rc;
     }
     c->epoch = 0;
+    c->hint[0] = c->hint[1] = -1;
     {
         // tuning override: fewer workgroups per CU than fit
         const char *g = getenv("QHUFF_GRID_WG_PER_CU");
@@ -840,6 +844,13 @@ pick_full(qhuff_ctx *c, int kind, Coord *k)
     k->rare = c->rare_dev + 2 * kind;
     if (c->kernels)
         return c->last_full[kind] = c->kernels == 2;
+    if (c->hint[kind] >= 0)
+    {
+        // the host path read this batch's offsets (host_hint): no history
+        const bool f = c->hint[kind] > 0;
+        c->hint[kind] = -1;
+        return c->last_full[kind] = f;
+    }
     volatile uint32_t *r = c->rare_host + 2 * kind;
     if (r[0])
     {
@@ -1082,6 +1093,44 @@ pipe_setup(qhuff_ctx *c)
     return QHUFF_OK;
 }
 
+// The variant the kernels' own rules call for on a batch whose offsets the
+// host holds (the host-memory paths): the full kernel when a string is
+// longer than kHintLen bytes (decode: the cooperative threshold, kCoopMin
+// Huffman bytes; encode: a payload the full emit copies with the whole
+// wave, at ~8 bits a byte) or a 64-string tile spans more than the 3 KB
+// stage can take (a big tile).  One pass over the offsets on the copy
+// workers.  VERDICT r04 item 2: the device-pointer calls can only go by
+// history; these need not.
+constexpr uint32_t kHintLen = 128;
+constexpr uint32_t kHintSpan = 3072 - 32;
+static bool
+host_rare(qhuff_ctx *c, const uint32_t *off, uint32_t n)
+{
+    std::atomic<bool> rare{false};
+    const uint32_t tiles = (n + 63) / 64, per = 1024;   // tiles per slice
+    c->pool->run((tiles + per - 1) / per, [&](unsigned k) {
+        const uint32_t t0 = k * per, t1 = t0 + per < tiles ? t0 + per : tiles;
+        bool r = false;
+        for (uint32_t t = t0; t < t1 && !r; ++t)
+        {
+            const uint32_t a = 64 * t, b = a + 64 < n ? a + 64 : n;
+            r = off[b] - off[a] > kHintSpan;
+            for (uint32_t i = a; i < b; ++i)
+                r |= off[i + 1] - off[i] > kHintLen;
+        }
+        if (r)
+            rare.store(true, std::memory_order_relaxed);
+    });
+    return rare.load();
+}
+
+static void
+host_hint(qhuff_ctx *c, bool enc, const uint32_t *off, uint32_t n)
+{
+    if (c->kernels == 0)
+        c->hint[enc ? 0 : 1] = host_rare(c, off, n) ? 1 : 0;
+}
+
 // The PCIe-inclusive path as a chunked pipeline.  The batch is cut into K
 // string ranges; per chunk: pinned staging copy (copy workers) -> H2D on the
 // upload stream -> kernel on the context stream (its out_off / status come
@@ -1163,6 +1212,7 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
         const uint8_t *din = D + o_in - a0;      // kernels see original offsets
         const uint32_t *doff = (const uint32_t *) (D + o_off) + s0;
         uint32_t *doo = (uint32_t *) (D + o_oo) + s0 + i;
+        host_hint(c, enc, in_off + s0, s1 - s0);
         int r = enc ? qhuff_encode_batch(c, din, doff, s1 - s0, mode,
                                          D + o_out + ob[i], doo, sk)
                     : qhuff_decode_batch(c, din, doff, s1 - s0,
@@ -1796,6 +1846,9 @@ qhuff_decode_literals_ex(qhuff_ctx *c, const uint8_t *buf,
     }
     if (nh)
     {
+        if (!c->pipe_ready && (rc = pipe_setup(c)))
+            return rc;
+        host_hint(c, false, hoff, nh);
         HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, o_out,
                                  hipMemcpyHostToDevice, st));
         rc = qhuff_decode_batch(c, c->d_stage, (const uint32_t *) (c->d_stage

@@ -453,6 +453,42 @@ def test_kernel_variant_switch():
         c.close()
 
 
+def test_host_path_variant_from_batch():
+    """Host-memory calls choose the kernel variant from the batch itself
+    (qhuff_host.cpp host_hint: the offsets are on the host): after 10 token
+    batches a batch with big tiles runs the full kernel on its first
+    launch, and the next token batch the lean one again -- no history, no
+    first-launch cliff (VERDICT r04 item 2 for the paths that can see their
+    offsets; device-pointer calls keep pick_full).  Outputs vs the oracle."""
+    import qhuff
+    if os.environ.get("QHUFF_KERNELS"):
+        pytest.skip("QHUFF_KERNELS pins the variant")
+    rng = random.Random(12)
+    big = []
+    for t in range(30):
+        big += rand_strings(rng, 62, ALPHAS["token"], 0, 20) \
+            + rand_strings(rng, 2, ALPHAS["token"], 150, 3500)
+    bdata, boff = pack(big)
+    sdata, soff = qhuff.synth_batch(1 << 13, seed=4)
+    c = qhuff.Codec(0)
+    try:
+        E, D = qhuff.KIND_ENCODE, qhuff.KIND_DECODE
+        for data, off, want in [(sdata, soff, 0)] * 10 + [(bdata, boff, 1),
+                                                         (sdata, soff, 0)]:
+            o_out, o_off = O.encode_batch(data, off, 0)
+            g_out, g_off = c.encode_host(data, off, 0)
+            assert np.array_equal(g_off, o_off)
+            assert np.array_equal(g_out[:o_off[-1]], o_out[:o_off[-1]])
+            h = o_out[:o_off[-1]].copy()
+            d_out, d_off, d_st = c.decode_host(h, o_off)
+            assert not d_st.any() and np.array_equal(d_off, off)
+            assert np.array_equal(d_out[:off[-1]], data)
+            assert (c.kernel_variant(E), c.kernel_variant(D)) == (want, want)
+        assert c.device_error() == 0
+    finally:
+        c.close()
+
+
 def test_small_grid_long_runs():
     """A grid of a few workgroups (QHUFF_GRID_PCT=4: ~10 of 256) over 4,096
     tiles: each wave codes ~34 tiles, so the ticket claims two iterations

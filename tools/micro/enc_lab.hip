@@ -29,7 +29,7 @@ enc_lab(EncArgs a, int reps, MbOut *res)
     const Span sp = tile_span(a.in, to.first(), to.last(), kStageCap);
     Chunks<kChunks> ch;
     ch.load(sp);
-    EncPolicy pol;
+    EncPolicyT<EncSmem, false> pol;
     pol.in = a.in;
     pol.mode = a.mode;
     pol.sm = sm;
