@@ -580,8 +580,11 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
     first_launch_us: each batch's first encode and
     first decode launch, timed right after 8 token launches of each kind on
     the same context -- no warm-up on the batch itself (the code objects are
-    loaded by the earlier legs); round 4's history-based kernel choice ran
-    that launch lean, 3.4 ms / 0.7 ms on the corpus."""
+    loaded by the earlier legs).  By history (enc / dec: the device-pointer
+    calls' default, qhuff_host.cpp pick_full) that launch runs lean, 3.4 ms
+    / 0.7 ms on the corpus; hinted_*: the same with the variant hinted from
+    the host's copy of the offsets (qhuff_batch_hint, as the host-memory
+    calls do themselves)."""
     from qhuff import workload as W
     K = 10
     data_dir = os.path.join(ROOT, "tests", "golden", "data")
@@ -644,6 +647,28 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
         var_d = codec.kernel_variant(qhuff.KIND_DECODE)
         codec.timing(False)
         first_ok = (torch.equal(do[:raw], d) and not bool(st.any()))
+        # the same with the variant hinted from the host copy of the batch's
+        # offsets (qhuff_batch_hint / qhuff_batch_needs_full, ABI 6)
+        hint = qhuff.batch_needs_full(off)
+        hint_d = qhuff.batch_needs_full(hoff)
+        hinted = {}
+        for kind, hv in ((qhuff.KIND_ENCODE, hint), (qhuff.KIND_DECODE, hint_d)):
+            for _ in range(8):
+                if kind == qhuff.KIND_ENCODE:
+                    codec.encode_into(s_in, s_off, n, 0, s_eo, s_eoo, stream)
+                else:
+                    codec.decode_into(s_h, s_hoff, n, s_do, s_doo, s_st, stream)
+            torch.cuda.synchronize()
+            codec.timing(True)
+            codec.batch_hint(kind, hv)
+            if kind == qhuff.KIND_ENCODE:
+                codec.encode_into(d, o, n, 0, eo, eoo, stream)
+            else:
+                codec.decode_into(h, eoo, n, do, doo, st, stream)
+            torch.cuda.synchronize()
+            hinted[kind] = [u for k, u in codec.timing_read() if k == kind][0]
+            codec.timing(False)
+        first_ok = first_ok and torch.equal(do[:raw], d) and not bool(st.any())
         for _ in range(2):
             codec.encode_into(d, o, n, 0, eo, eoo, stream)
             codec.decode_into(h, eoo, n, do, doo, st, stream)
@@ -671,7 +696,13 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
                                    "dec": round(first_d[0], 2),
                                    "enc_vs_mean": round(first_e[0] / e_us, 3),
                                    "dec_vs_mean": round(first_d[0] / d_us, 3),
-                                   "full_loop": [var_e, var_d],
+                                   "full_kernel": [var_e, var_d],
+                                   "hinted_enc": round(hinted[qhuff.KIND_ENCODE], 2),
+                                   "hinted_dec": round(hinted[qhuff.KIND_DECODE], 2),
+                                   "hinted_vs_mean": [
+                                       round(hinted[qhuff.KIND_ENCODE] / e_us, 3),
+                                       round(hinted[qhuff.KIND_DECODE] / d_us, 3)],
+                                   "hint": [hint, hint_d],
                                    "roundtrip_ok": bool(first_ok)},
                "roundtrip_ok": bool(ok)}
         ent.update(W.tile_shares(data, off, hoff))

@@ -51,7 +51,8 @@ extern "C" {
  *      qhuff_timing_enable(ctx, k > 1) samples every k-th launch
  *   6  QHUFF_MAX_STRLEN: qhuff_scan_field_section rejects (QHUFF_EPROTO) a
  *      literal whose declared length exceeds it; qhuff_decode_literals_ex
- *      rejects a literal whose decoded length does */
+ *      rejects a literal whose decoded length does; qhuff_batch_hint /
+ *      qhuff_batch_needs_full (the kernel variant from the batch) */
 #define QHUFF_ABI_VERSION 6
 
 /* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
@@ -410,6 +411,21 @@ int qhuff_timing_read(qhuff_ctx *ctx, uint32_t *kind, double *us, uint32_t max);
  * lean one or none yet, QHUFF_EINVAL otherwise.  Diagnostic: the output
  * bytes are the same either way. */
 int qhuff_kernel_variant(qhuff_ctx *ctx, int kind);
+
+/* (ABI 6) The variant of the next launch of `kind` from what the caller
+ * knows of its batch, instead of the history above: hint 1 = the batch has
+ * a string longer than 128 bytes or a 64-string tile spanning more than the
+ * kernels' 3 KB stage (the full kernel), 0 = it has none (the lean one),
+ * -1 = no hint.  Applies to the next launch of that kind only.  The host-
+ * memory calls (qhuff_*_batch_host, qhuff_decode_literals_*) set it
+ * themselves from the offsets they hold; a caller of the device-pointer
+ * calls that keeps a host copy of its offsets (e.g. from
+ * qhuff_scan_field_section) can compute it with qhuff_batch_needs_full. */
+int qhuff_batch_hint(qhuff_ctx *ctx, int kind, int hint);
+
+/* 1 if host offsets in_off[n + 1] describe a batch the full kernel is for
+ * (the rule above), 0 if not, QHUFF_EINVAL for a null pointer.  Host only. */
+int qhuff_batch_needs_full(const uint32_t *in_off, uint32_t n);
 
 /* ---- multi-GPU sharding helpers (host arithmetic only) ----------------
  * Byte-balanced contiguous partition of a batch into g shards: writes

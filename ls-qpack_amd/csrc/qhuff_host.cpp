@@ -1131,6 +1131,33 @@ host_hint(qhuff_ctx *c, bool enc, const uint32_t *off, uint32_t n)
         c->hint[enc ? 0 : 1] = host_rare(c, off, n) ? 1 : 0;
 }
 
+extern "C" int
+qhuff_batch_hint(qhuff_ctx *c, int kind, int hint)
+{
+    if (!c || (kind != QHUFF_KIND_ENCODE && kind != QHUFF_KIND_DECODE)
+            || hint < -1 || hint > 1)
+        return QHUFF_EINVAL;
+    c->hint[kind] = hint;
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_batch_needs_full(const uint32_t *off, uint32_t n)
+{
+    if (!off)
+        return QHUFF_EINVAL;
+    for (uint32_t a = 0; a < n; a += 64)
+    {
+        const uint32_t b = a + 64 < n ? a + 64 : n;
+        if (off[b] - off[a] > kHintSpan)
+            return 1;
+        for (uint32_t i = a; i < b; ++i)
+            if (off[i + 1] - off[i] > kHintLen)
+                return 1;
+    }
+    return 0;
+}
+
 // The PCIe-inclusive path as a chunked pipeline.  The batch is cut into K
 // string ranges; per chunk: pinned staging copy (copy workers) -> H2D on the
 // upload stream -> kernel on the context stream (its out_off / status come

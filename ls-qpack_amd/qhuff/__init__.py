@@ -32,7 +32,7 @@ EXPORTS = (
     "qhuff_xxh32_headers", "qhuff_xxh32_batch",
     "qhuff_scan_field_section", "qhuff_scan_encoder_stream",
     "qhuff_literals_bound", "qhuff_decode_literals_host",
-    "qhuff_decode_literals_ex",
+    "qhuff_decode_literals_ex", "qhuff_batch_hint", "qhuff_batch_needs_full",
     "qhuff_frame_literal", "qhuff_xxh32_headers_host",
     "qhuff_svc_open", "qhuff_svc_close", "qhuff_svc_encode",
     "qhuff_svc_decode", "qhuff_svc_stats",
@@ -199,6 +199,10 @@ def lib():
         L.qhuff_timing_enable.argtypes = [vp, C.c_int]
         L.qhuff_kernel_variant.restype = C.c_int
         L.qhuff_kernel_variant.argtypes = [vp, C.c_int]
+        L.qhuff_batch_hint.restype = C.c_int
+        L.qhuff_batch_hint.argtypes = [vp, C.c_int, C.c_int]
+        L.qhuff_batch_needs_full.restype = C.c_int
+        L.qhuff_batch_needs_full.argtypes = [u32p, C.c_uint32]
         L.qhuff_timing_read.restype = C.c_int
         L.qhuff_timing_read.argtypes = [vp, u32p, C.POINTER(C.c_double),
                                         C.c_uint32]
@@ -235,6 +239,14 @@ def shard_cuts(in_off, g):
     if rc:
         raise QhuffError("qhuff_shard_cuts: %d" % rc)
     return cuts
+
+
+def batch_needs_full(in_off):
+    """qhuff_batch_needs_full: 1 if host offsets describe a batch the full
+    kernel is for (a string > 128 bytes or a tile past the 3 KB stage)."""
+    import numpy as np
+    in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
+    return int(lib().qhuff_batch_needs_full(_np_ptr(in_off), len(in_off) - 1))
 
 
 def _scan(fn, buf, pos_base, *extra):
@@ -377,6 +389,12 @@ class Codec:
         if r < 0:
             self._check(r, "qhuff_kernel_variant")
         return r
+
+    def batch_hint(self, kind, hint):
+        """qhuff_batch_hint: the next launch of kind runs the full (1) or
+        lean (0) kernel, or by history (-1)."""
+        self._check(lib().qhuff_batch_hint(self._ctx, kind, hint),
+                    "qhuff_batch_hint")
 
     def timing_read(self, max_launches=TIMING_SLOTS):
         """qhuff_timing_read -> list of (kind, microseconds) of the launches

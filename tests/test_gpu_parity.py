@@ -489,6 +489,38 @@ def test_host_path_variant_from_batch():
         c.close()
 
 
+def test_device_batch_hint():
+    """qhuff_batch_hint on the device-pointer calls: with the hint computed
+    from the caller's host copy of the offsets (qhuff_batch_needs_full) a
+    big-tile batch runs the full kernel on its first launch after token
+    launches, and a hinted token batch the lean one; outputs exact."""
+    import qhuff
+    if os.environ.get("QHUFF_KERNELS"):
+        pytest.skip("QHUFF_KERNELS pins the variant")
+    rng = random.Random(13)
+    big = []
+    for t in range(30):
+        big += rand_strings(rng, 63, ALPHAS["token"], 0, 20) \
+            + rand_strings(rng, 1, ALPHAS["token"], 3200, 5000)
+    bdata, boff = pack(big)
+    sdata, soff = qhuff.synth_batch(1 << 14, seed=3)
+    c = qhuff.Codec(0)
+    try:
+        E = qhuff.KIND_ENCODE
+        for _ in range(8):
+            c.batch_hint(E, qhuff.batch_needs_full(soff))
+            check_encode(c, sdata, soff, 0)
+            assert c.kernel_variant(E) == 0
+        c.batch_hint(E, qhuff.batch_needs_full(boff))
+        check_encode(c, bdata, boff, 0)
+        assert c.kernel_variant(E) == 1
+        c.batch_hint(E, qhuff.batch_needs_full(soff))
+        check_encode(c, sdata, soff, 0)
+        assert c.kernel_variant(E) == 0
+    finally:
+        c.close()
+
+
 def test_small_grid_long_runs():
     """A grid of a few workgroups (QHUFF_GRID_PCT=4: ~10 of 256) over 4,096
     tiles: each wave codes ~34 tiles, so the ticket claims two iterations

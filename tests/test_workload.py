@@ -64,3 +64,21 @@ def test_long_and_big_tiles_are_counted():
     assert sh["decode_slow_tile_share"] == round(1 / 3, 4)
     assert sh["encode_slow_tile_share"] == round(1 / 3, 4)
     assert sh["encode_coop_tile_share"] == round(1 / 3, 4)
+
+
+def test_batch_needs_full():
+    """qhuff_batch_needs_full (host only): the full kernel for a batch with a
+    string above 128 bytes or a 64-string tile past the 3 KB stage (the
+    kernels' own big-tile / long-string rules), not for the token batch."""
+    import numpy as np
+    import qhuff
+    data, off = qhuff.synth_batch(1 << 14, seed=9)
+    assert qhuff.batch_needs_full(off) == 0
+    lens = np.diff(off.astype(np.int64))
+    lens[700] = 129
+    assert qhuff.batch_needs_full(np.concatenate([[0], np.cumsum(lens)])) == 1
+    lens[700] = 128
+    assert qhuff.batch_needs_full(np.concatenate([[0], np.cumsum(lens)])) == 0
+    big = np.full(64, 48, dtype=np.int64)               # a 3,072-byte tile
+    assert qhuff.batch_needs_full(np.concatenate([[0], np.cumsum(big)])) == 1
+    assert qhuff.batch_needs_full(np.zeros(1, np.uint32)) == 0
