@@ -499,8 +499,12 @@ write_bytes(QH_LDS uint8_t *d, uint32_t v, uint32_t nb)
 #endif
 constexpr uint32_t kCoopMin = QH_COOP_MIN;      // Huffman bytes
 #ifndef QH_SEG_MIN
-#define QH_SEG_MIN 128
+#define QH_SEG_MIN 64
 #endif
+// (round 5: 64, was 128 -- a tile whose long strings total under ~8k bits
+// spreads them over twice the lanes; corpus decode 0.95x in 8 same-box
+// pairs, 32 and the thresholds 96 / 160 / 192 no better,
+// profiles/r05_coopsweep)
 constexpr uint32_t kSegMin = QH_SEG_MIN;        // bits per segment
 static_assert(kSegMin % 32 == 0 && kSegMin >= 64, "segment bits");
 constexpr uint32_t kCoopDummy = 128;            // sink bytes, 2 per lane

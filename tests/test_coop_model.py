@@ -19,7 +19,7 @@ import _paths  # noqa: F401
 import oracle_lib as O
 
 G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "data")
-SEG_MIN = 128                                # kSegMin (bits)
+SEG_MIN = 64                                 # kSegMin (bits)
 
 
 def _codes():

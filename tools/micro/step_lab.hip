@@ -85,6 +85,62 @@ struct AddtidEmit
     }
 };
 
+//  each lane's output bytes packed in a register and
+// written one dword at a time: every step ORs its nb bytes into the dword
+// being filled and stores that dword (partial or full, ONE ds_write_b32 per
+// step instead of two ds_write_b8), moving on a dword when it is full.  The
+// lane's slot must start on a dword (sl % 4 == 0).
+struct PackEmit
+{
+    QH_LDS uint32_t *slot, *p;
+    uint32_t acc;                    // bytes of *p so far (sh / 8 of them)
+    uint32_t sh;                     // 8 * bytes in acc
+    uint32_t n;
+    __device__ __forceinline__ void finish() {}
+    __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
+    {
+        // sym0 [7:0], sym1 [23:16] -> bytes 0, 1; only nb of them
+        uint32_t two = __builtin_amdgcn_perm(val, val, 0x0c0c0200u);
+        two = __builtin_amdgcn_ubfe(two, 0, 8 * nb);
+        const uint32_t v = acc | (two << sh);
+        *p = v;
+        const uint32_t s2 = sh + 8 * nb;
+        const bool full = s2 >= 32;
+        const uint32_t carry = sh ? two >> ((32 - sh) & 31) : 0u;
+        acc = full ? carry : v;
+        p += full ? 1 : 0;
+        sh = s2 & 31;
+        n += nb;
+    }
+};
+// the same, the store only when the dword is full (exec-masked), the
+// partial dword once at the end
+struct PackEmitM
+{
+    QH_LDS uint32_t *slot, *p;
+    uint32_t acc, sh, n;
+    __device__ __forceinline__ void finish()
+    {
+        if (sh)
+            *p = acc;
+    }
+    __device__ __forceinline__ void operator()(uint32_t val, uint32_t nb)
+    {
+        uint32_t two = __builtin_amdgcn_perm(val, val, 0x0c0c0200u);
+        two = __builtin_amdgcn_ubfe(two, 0, 8 * nb);
+        const uint32_t v = acc | (two << sh);
+        const uint32_t s2 = sh + 8 * nb;
+        const bool full = s2 >= 32;
+        if (full)
+            *p = v;
+        const uint32_t carry = sh ? two >> ((32 - sh) & 31) : 0u;
+        acc = full ? carry : v;
+        p += full ? 1 : 0;
+        sh = s2 & 31;
+        n += nb;
+    }
+};
+
 struct MbOut { unsigned long long cyc, steps, sum; };
 
 template <int W, int MODE>
@@ -160,6 +216,31 @@ lab(DecArgs a, int reps, MbOut *res)
             n = MODE == 9
                 ? decode_string_lds<ArenaEmit, false>(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em)
                 : decode_string_lds<ArenaEmit, true>(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
+        }
+        else if (MODE == 12 || MODE == 13 || MODE == 14 || MODE == 15)
+        {
+            // packed dwords: fixed stride 108 (12, 13) or the kernel's
+            // variable slots rounded up to a dword (14, 15; 4 bytes of
+            // slack per lane instead of 2)
+            const uint32_t sl = MODE <= 13 ? 108 * lane
+                              : (4 * lane + (uint32_t) ((8ull * (to.o0 - A0)) / 5) + 3) & ~3u;
+            QH_LDS uint32_t *q = (QH_LDS uint32_t *) (wv->arena + sl);
+            if (MODE == 12 || MODE == 14)
+            {
+                PackEmit em{q, q, 0, 0, 0};
+                n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
+            }
+            else
+            {
+                PackEmitM em{q, q, 0, 0, 0};
+                n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
+            }
+        }
+        else if (MODE == 16)
+        {
+            // the kernel's sink in the kernel's variable slots
+            ArenaEmit em{wv->arena + slot0, wv->arena + slot0, 0};
+            n = decode_string_lds(wv->in, 8 * rs, 8 * re, sm->win, sm->sorted, sm->long2, em);
         }
         else
         {
@@ -359,6 +440,22 @@ int main(int argc, char **argv)
     DecArgs a = {};
     a.in = d_h; a.in_off = d_ho; a.win = d_win; a.sorted = d_sorted; a.n = n;
     a.c.n_tiles = n / 64;
+    if (argc > 2 && argv[2][0] == 'p')
+    {
+        // the packed-dword sink against the kernel's,
+        // interleaved
+        for (int k = 0; k < 3; ++k)
+        {
+            run<12, 16>("arena b8x2 var", a, reps);
+            run<12, 14>("pack b32 var", a, reps);
+            run<12, 15>("packM b32 var", a, reps);
+            run<12, 10>("arena b8x2 108", a, reps);
+            run<12, 12>("pack b32 108", a, reps);
+            run<12, 13>("packM b32 108", a, reps);
+            run<12, 1>("no store", a, reps);
+        }
+        return 0;
+    }
     if (argc > 2)
     {
         // the refill A/B only, interleaved
