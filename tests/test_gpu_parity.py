@@ -343,6 +343,33 @@ def test_decode_cooperative_long_strings(codec, alpha):
     check_decode(codec, data, off, pad_front=7)
 
 
+def test_decode_cooperative_many_per_tile(codec):
+    """Tiles holding 2-12 cooperative strings of 130-900 Huffman bytes
+    (several strings share the 64 lanes; S from their total, down to the
+    64-bit segment minimum) in random places among short ones, a few of
+    them invalid; statuses and bytes against the oracle."""
+    rng = random.Random(777)
+    strs = []
+    for t in range(48):
+        k = rng.randrange(2, 13)
+        longs = set(rng.sample(range(64), k))
+        for i in range(64):
+            if i in longs:
+                s = bytes(rng.choice(ALPHAS["token"])
+                          for _ in range(rng.randrange(175, 1200)))
+                h = bytearray(O.huffman_enc(s))
+                if rng.random() < 0.08:                  # an invalid one
+                    h[rng.randrange(len(h))] ^= 1 << rng.randrange(8)
+                strs.append(bytes(h))
+            else:
+                strs.append(O.huffman_enc(
+                    bytes(rng.choice(ALPHAS["token"])
+                          for _ in range(rng.randrange(0, 40)))))
+    data, off = pack(strs)
+    out, oo, st = check_decode(codec, data, off)
+    assert (st == 0).sum() > 2900
+
+
 def test_decode_cooperative_invalid(codec):
     """Invalid long strings (an EOS code inside, a flipped bit, non-ones or
     over-long padding, a cut string) take the one-lane decode again: status
@@ -400,6 +427,7 @@ def test_kernel_variants(kernels):
             test_big_tile_slots(c)
             test_multi_unit_tiles(c, 100, 400)
             test_decode_cooperative_long_strings(c, "token")
+            test_decode_cooperative_many_per_tile(c)
             test_decode_cooperative_invalid(c)
             for mode in (0, 7):
                 check_encode(c, *mixed, mode)
