@@ -947,15 +947,15 @@ template <bool Keep, class SM, class BaseOf>
 __device__ __noinline__ uint64_t
 dec_slow_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
               uint32_t slot0, uint32_t cnt, TileOffs to, Span sp, uint32_t sz,
-              uint32_t st, uint8_t *out, uint32_t *t_off, uint8_t *t_status,
-              BaseOf base_of)
+              uint32_t st, bool sized, uint8_t *out, uint32_t *t_off,
+              uint8_t *t_status, BaseOf base_of)
 {
     const uint32_t lane = lane_id();
     const bool valid = lane < cnt;
     const uint32_t rs = valid ? (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa) : 0;
     const uint32_t re = valid ? (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa) : 0;
     const DecGlb src{(const QH_GLB uint32_t *) sp.pa};
-    if (!sp.staged)
+    if (!sp.staged && !sized)
     {
         int r = 0;
         if (valid)
@@ -990,6 +990,33 @@ dec_slow_tile(const uint8_t *in, QH_LDS SM *sm, QH_LDS DecWave *wv,
     return base + total;
 }
 
+
+// The sizes (and statuses) of a tile past the stage, counted in global
+// memory, as dec_slow_tile counts them (sized = false)
+struct SzSt
+{
+    uint32_t sz, st;
+};
+template <bool Keep, class SM>
+__device__ __noinline__ SzSt
+dec_tile_sizes(const uint8_t *in, QH_LDS SM *sm, uint32_t cnt, TileOffs to,
+               Span sp)
+{
+    const bool valid = lane_id() < cnt;
+    int r = 0;
+    if (valid)
+    {
+        const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
+        const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
+        const DecGlb src{(const QH_GLB uint32_t *) sp.pa};
+        CountEmit em{0};
+        r = decode_string(src, 8 * rs, 8 * re, sm->win, sm->sorted, em);
+    }
+    SzSt o;
+    o.sz = r >= 0 ? (uint32_t) r : Keep ? (uint32_t) (-1 - r) : 0u;
+    o.st = r < 0 ? QHUFF_DEC_ERROR : QHUFF_DEC_OK;
+    return o;
+}
 
 template <bool Keep, class SM>
 __device__ __forceinline__ bool
@@ -1176,17 +1203,27 @@ struct DecPolicyT
     }
     // a big tile whose output does not fit a slot (qhuff_pipeline.h), after
     // the pending tiles are flushed: base from the look-back
+    // the sizes of a tile past the stage (the lean kernel: no codec ran)
+    __device__ __forceinline__ void slow_size(uint32_t cnt, Offs to, Span sp,
+                                              uint32_t &sz, uint32_t &st)
+    {
+        const SzSt r = dec_tile_sizes<Keep>(in, sm, cnt, to, sp);
+        sz = r.sz;
+        st = r.st;
+    }
+    // ... its output once the look-back lb (aggregate published) resolves
     __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
                                               Offs to, Span sp, uint32_t sz,
-                                              uint32_t st, uint8_t *out,
-                                              uint32_t *out_off, uint8_t *status,
-                                              uint64_t n)
+                                              uint32_t st, bool sized,
+                                              uint8_t *out, uint32_t *out_off,
+                                              uint8_t *status, uint64_t n,
+                                              const LookBack &lb)
     {
         const uint64_t s0 = (uint64_t) t * kTS;
         const uint64_t end = dec_slow_tile<Keep>(in, sm, wv, slot0, cnt, to,
-                                                    sp, sz, st, out, out_off + s0,
-                                                    status + s0,
-                                                    LookBackBase{c, t});
+                                                    sp, sz, st, sized, out,
+                                                    out_off + s0, status + s0,
+                                                    StartedBase{c, lb});
         last_tile_end(c, t, end, out_off, n);
     }
     // a tile at a known base
@@ -1197,7 +1234,8 @@ struct DecPolicyT
                                                      uint8_t *t_status)
     {
         return dec_slow_tile<Keep>(in, sm, wv, slot0, cnt, to, sp, sz, st,
-                                      out, t_off, t_status, FixedBase{base});
+                                      false, out, t_off, t_status,
+                                      FixedBase{base});
     }
 };
 

@@ -709,8 +709,8 @@ template <class SM, class BaseOf>
 __device__ __noinline__ uint64_t
 enc_slow_tile(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
               QH_LDS EncWave *wv, uint32_t rs, uint32_t re, EncSize z,
-              uint32_t cnt, TileOffs to, Span sp, uint32_t sz, uint8_t *out,
-              uint32_t *t_off, BaseOf base_of)
+              uint32_t cnt, TileOffs to, Span sp, uint32_t sz, bool sized,
+              uint8_t *out, uint32_t *t_off, BaseOf base_of)
 {
     const uint32_t lane = lane_id();
     const bool valid = lane < cnt;
@@ -719,10 +719,13 @@ enc_slow_tile(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
     {
         rs = valid ? (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa) : 0;
         re = valid ? (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa) : 0;
-        z = (EncSize){0, 0, true};
-        if (valid)
-            z = size_string(mode, gsrc, rs, re, sm->len);
-        sz = z.size;
+        if (!sized)
+        {
+            z = (EncSize){0, 0, true};
+            if (valid)
+                z = size_string(mode, gsrc, rs, re, sm->len);
+            sz = z.size;
+        }
     }
     const uint32_t incl = wave_incl_scan(sz);
     const uint32_t excl = incl - sz;
@@ -746,6 +749,24 @@ enc_slow_tile(const uint8_t *in, uint32_t mode, QH_LDS SM *sm,
     return base + total;
 }
 
+
+// the sizes of a tile past the stage, from global memory (as enc_slow_tile
+// sizes them with sized = false)
+template <class SM>
+__device__ __noinline__ EncSize
+enc_tile_sizes(const uint8_t *in, uint32_t mode, QH_LDS SM *sm, uint32_t cnt,
+               TileOffs to, Span sp)
+{
+    EncSize z = (EncSize){0, 0, true};
+    if (lane_id() < cnt)
+    {
+        const EncGlb gsrc{(const QH_GLB uint32_t *) sp.pa};
+        const uint32_t rs = (uint32_t) ((uintptr_t) (in + to.o0) - sp.pa);
+        const uint32_t re = (uint32_t) ((uintptr_t) (in + to.o1) - sp.pa);
+        z = size_string(mode, gsrc, rs, re, sm->len);
+    }
+    return z;
+}
 
 template <class SM>
 __device__ __forceinline__ bool
@@ -902,16 +923,27 @@ struct EncPolicyT
     }
     // a big tile whose output does not fit a slot (qhuff_pipeline.h), after
     // the pending tiles are flushed: base from the look-back
+    // the sizes of a tile past the stage (the lean kernel: no codec ran)
+    __device__ __forceinline__ void slow_size(uint32_t cnt, TileOffs to, Span sp,
+                                              uint32_t &sz, uint32_t &st)
+    {
+        z = enc_tile_sizes(in, mode, sm, cnt, to, sp);
+        sz = z.size;
+        st = 0;
+    }
+    // ... its output once the look-back lb (aggregate published) resolves
     __device__ __forceinline__ void slow_tile(Coord c, uint32_t t, uint32_t cnt,
                                               TileOffs to, Span sp, uint32_t sz,
-                                              uint32_t, uint8_t *out,
+                                              uint32_t, bool sized, uint8_t *out,
                                               uint32_t *out_off, uint8_t *,
-                                              uint64_t n)
+                                              uint64_t n, const LookBack &lb)
     {
+        // sized: z from slow_size (the lean kernel) -- a full kernel's big
+        // tile has its sizes from big_sizes but not z, so it sizes again
         const uint64_t end = enc_slow_tile(in, mode, sm, wv, rs, re, z, cnt,
-                                              to, sp, sz, out,
+                                              to, sp, sz, sized, out,
                                               out_off + (uint64_t) t * kTS,
-                                              LookBackBase{c, t});
+                                              StartedBase{c, lb});
         last_tile_end(c, t, end, out_off, n);
     }
     // a tile at a known base
@@ -921,7 +953,7 @@ struct EncPolicyT
                                                      uint8_t *out, uint32_t *t_off,
                                                      uint8_t *)
     {
-        return enc_slow_tile(in, mode, sm, wv, rs, re, z, cnt, to, sp, sz,
+        return enc_slow_tile(in, mode, sm, wv, rs, re, z, cnt, to, sp, sz, false,
                                 out, t_off, FixedBase{base});
     }
 };

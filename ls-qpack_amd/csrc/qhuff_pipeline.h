@@ -101,6 +101,19 @@ struct LookBackBase
         return lb.finish(c);
     }
 };
+// ... or a look-back already started (its aggregate published, its super
+// add returned: the batch kernel's slow tiles, published before the wave's
+// pending tiles are flushed)
+struct StartedBase
+{
+    Coord c;
+    LookBack lb;
+    __device__ __forceinline__ uint64_t operator()(uint32_t)
+    {
+        lb.poll(c);
+        return lb.finish(c);
+    }
+};
 struct FixedBase
 {
     uint64_t base;
@@ -653,10 +666,21 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         else
         {
             rare = true;
-            // (rare: a big tile whose output exceeds a slot -- or, with
-            // QH_BIG_TILES 0, every big tile -- coded out of line after the
-            // pending tiles are flushed, so that no tile output is live across
-            // the call)
+            // (rare: a big tile in the lean kernel, or one whose output
+            // exceeds a slot) coded out of line after the pending tiles are
+            // flushed, so that no tile output is live across the call -- but
+            // its sizes first and its aggregate published BEFORE those
+            // flushes wait on anything (round 5): the flushes wait on earlier
+            // tiles, big ones among them, and a big tile that published only
+            // after its own flushes chained every big tile of the batch
+            // behind the one before it (the lean kernels' first launch on the
+            // QIF corpus: encode ~3 ms against 70 us)
+            if constexpr (!P::kBig)
+                if (!sp_cur.staged)
+                    pol.slow_size(cnt, o_cur, sp_cur, sz, st);
+            LookBack lbb;
+            lbb.start(c, t, read_lane(wave_incl_scan(sz), 63));
+            lbb.super_agg(c);
 #pragma unroll
             for (int i = 0; i < D; ++i)
                 if (pend[i].valid)
@@ -666,8 +690,8 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
                     flush_at(i, l, ~0u);
                 }
             prof_stamp(c, kProfIters - 1, 0);    // (profiling) big tile
-            pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, out, out_off,
-                          status, n);
+            pol.slow_tile(c, t, cnt, o_cur, sp_cur, sz, st, !P::kBig, out,
+                          out_off, status, n, lbb);
             prof_stamp(c, kProfIters - 1, 3);
         }
         wave_sync();
