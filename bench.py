@@ -579,10 +579,11 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
     (qhuff/workload.py: slow tiles, variable arena slots, encode fallback).
     first_launch_us: each batch's first encode and
     first decode launch, timed right after 8 token launches of each kind on
-    the same context -- no warm-up on the batch itself (the code objects are
-    loaded by the earlier legs).  By history (enc / dec: the device-pointer
-    calls' default, qhuff_host.cpp pick_full) that launch runs lean, 3.4 ms
-    / 0.7 ms on the corpus; hinted_*: the same with the variant hinted from
+    the same context -- no launch on the batch itself before it (its
+    Huffman form is made on a second context; the code objects are loaded
+    by the earlier legs).  By history (enc / dec: the device-pointer calls'
+    default, qhuff_host.cpp pick_full) that launch runs lean, ~2.6 ms /
+    ~0.7 ms on the corpus; hinted_*: the same with the variant hinted from
     the host's copy of the offsets (qhuff_batch_hint, as the host-memory
     calls do themselves)."""
     from qhuff import workload as W
@@ -608,6 +609,11 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
     syn_gbps = 2 * raw_syn / ((enc_ms_syn + dec_ms_syn) * 1e-3) / 1e9
     out = {"strings": n, "launches_per_kernel": K,
            "synthetic_token_gbps": round(syn_gbps, 1)}
+    # each batch's Huffman form (the decode legs' input) made on a context
+    # of its own: on `codec` that launch would be a launch on the batch
+    # before its first-launch measurement (its rare-tile report sets the
+    # variant history)
+    prep = qhuff.Codec(dev.index or 0)
     for name, desc, (data, off) in batches:
         raw = int(off[-1])
         d = torch.from_numpy(data).to(dev)
@@ -615,7 +621,7 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
         ecap = qhuff.encode_bound(raw, n, 0)
         eo = torch.empty(ecap, dtype=torch.uint8, device=dev)
         eoo = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        codec.encode_into(d, o, n, 0, eo, eoo, stream)
+        prep.encode_into(d, o, n, 0, eo, eoo, stream)
         torch.cuda.synchronize()
         hoff = eoo.cpu().numpy().view(np.uint32).copy()
         hb = int(hoff[-1])
@@ -625,12 +631,14 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
         doo = torch.empty(n + 1, dtype=torch.int32, device=dev)
         st = torch.empty(n, dtype=torch.uint8, device=dev)
         # the first launch of each kind on this batch, after 8 token
-        # launches of each kind (the output is checked with the others')
+        # launches of each kind, each waited for (the history counts
+        # launches seen to have run; the output is checked with the others')
         for _ in range(8):
             codec.encode_into(s_in, s_off, n, 0, s_eo, s_eoo, stream)
+            torch.cuda.synchronize()
         for _ in range(8):
             codec.decode_into(s_h, s_hoff, n, s_do, s_doo, s_st, stream)
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
         codec.timing(True)
         codec.encode_into(d, o, n, 0, eo, eoo, stream)
         torch.cuda.synchronize()
@@ -639,7 +647,7 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
         codec.timing(False)
         for _ in range(8):
             codec.decode_into(s_h, s_hoff, n, s_do, s_doo, s_st, stream)
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
         codec.timing(True)
         codec.decode_into(h, eoo, n, do, doo, st, stream)
         torch.cuda.synchronize()
@@ -658,7 +666,7 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
                     codec.encode_into(s_in, s_off, n, 0, s_eo, s_eoo, stream)
                 else:
                     codec.decode_into(s_h, s_hoff, n, s_do, s_doo, s_st, stream)
-            torch.cuda.synchronize()
+                torch.cuda.synchronize()
             codec.timing(True)
             codec.batch_hint(kind, hv)
             if kind == qhuff.KIND_ENCODE:
@@ -709,6 +717,7 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
         out[name] = ent
         del d, o, eo, eoo, h, do, doo, st
     del s_eo, s_eoo, s_do, s_doo, s_st
+    prep.close()
     return out
 
 
