@@ -403,10 +403,12 @@ int qhuff_timing_read(qhuff_ctx *ctx, uint32_t *kind, double *us, uint32_t max);
 
 /* Kernel variants.  Encode and decode each have a lean kernel and a full
  * one that also carries the big-tile slots and the cooperative long-string
- * decode; by default (QHUFF_KERNELS=auto) a context launches the lean one
- * until a launch of that kind reports such tiles, then the full one until
- * 8 launches have been seen to run without any (QHUFF_KERNELS=lean|full
- * pins one).  Returns 1 if the context's last launch of `kind`
+ * decode.  By default (QHUFF_KERNELS=auto) the variant comes from the batch
+ * when the library or the caller knows it (the host-memory calls; a hint,
+ * below); otherwise encode launches its full kernel, and decode the lean
+ * one until a launch reports such tiles, then the full one until 8
+ * launches have been seen to run without any (QHUFF_KERNELS=lean|full pins
+ * one).  Returns 1 if the context's last launch of `kind`
  * (QHUFF_KIND_ENCODE / QHUFF_KIND_DECODE) ran the full kernel, 0 if the
  * lean one or none yet, QHUFF_EINVAL otherwise.  Diagnostic: the output
  * bytes are the same either way. */

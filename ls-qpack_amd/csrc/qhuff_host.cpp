@@ -838,6 +838,13 @@ grid_for(const qhuff_ctx *c, uint64_t tiles, uint64_t waves_per_block,
 // such tile, then full -- was built three ways in round 5 and measured
 // slower: DESIGN.md section 6.)
 static constexpr uint32_t kCalm = 8;
+// (round 5) without a hint, encode runs its full kernel: on the token batch
+// it costs +1.3 % against the lean one (the full kernels' rare branches
+// marked cold, qhuff_pipeline.h QH_RARE), while the lean one's first launch
+// on a long-string batch took 30x its warmed time (the QIF corpus, 2.1 ms:
+// big tiles out of line, one lane per string in global memory); decode
+// keeps the history (full +3.3 %, lean first launch 4.1x)
+static constexpr bool kHistory[2] = {false, true};
 static bool
 pick_full(qhuff_ctx *c, int kind, Coord *k)
 {
@@ -851,6 +858,8 @@ pick_full(qhuff_ctx *c, int kind, Coord *k)
         c->hint[kind] = -1;
         return c->last_full[kind] = f;
     }
+    if (!kHistory[kind])
+        return c->last_full[kind] = true;
     volatile uint32_t *r = c->rare_host + 2 * kind;
     if (r[0])
     {

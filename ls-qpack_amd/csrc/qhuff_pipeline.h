@@ -51,6 +51,13 @@ namespace qhuff {
 #define QH_TAIL_STOP 6
 #endif
 
+// a rare branch of the full kernels' tile loop (their cooperative phase,
+// big tiles): marked cold there, so that block and spill placement favour
+// the loop (full kernels on the token batch: encode 0.955, decode 0.982,
+// profiles/r05_cold); the lean kernels' loop is left as it was (the same
+// hints cost their decode ~1 %)
+#define QH_RARE(full, c) ((full) ? __builtin_expect((c), 0) : (c))
+
 constexpr int kChunks = 3;                  // 16-byte input chunks per lane
 constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: chunk registers / stages
 
@@ -562,7 +569,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         {
             pol.prepare(sp_cur);
             pol.codec(o_cur, cnt, sp_cur, &sz, &st);
-            if (P::kCoop && pol.coop)
+            if (QH_RARE(P::kBig, P::kCoop && pol.coop))
             {
                 park();
                 pol.coop_phase(o_cur, 0, cnt, sp_cur, &sz, &st);
@@ -581,7 +588,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
             // (P::big_sizes).  When it fits, it is pending like any other tile
             // from here on -- its output copied from the slot when its look-back
             // resolves -- and the wave goes straight on to its next tile.
-            if (!fast)
+            if (QH_RARE(P::kBig, !fast))
             {
                 rare = true;
                 // the pending tiles' outputs move to slots first, so that their
@@ -659,7 +666,7 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         pend[D - 1] = cur;
         prof_stamp(c, it, 5);
 
-        if (fast)
+        if (!QH_RARE(P::kBig, !fast))
             outs[D - 1].gather(pol.out_stage());
         else if (bigslot)
             outs[D - 1].clear();             // (its output is in its slot)

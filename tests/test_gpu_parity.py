@@ -440,12 +440,14 @@ def test_kernel_variants(kernels):
 
 
 def test_kernel_variant_switch():
-    """QHUFF_KERNELS=auto (qhuff_host.cpp pick_full): token batches run the
-    lean kernel; a batch with big tiles reports them and the next launch of
-    that kind runs the full one; after 8 launches seen to run without such
-    tiles the lean one again -- counted on launches that ran, so a burst of
-    issued launches does not flip it back (each launch here is synchronised,
-    as the slowest case).  Outputs checked against the oracle throughout."""
+    """QHUFF_KERNELS=auto (qhuff_host.cpp pick_full), device-pointer calls
+    without a hint: encode always runs its full kernel (round 5); decode's
+    token batches run the lean kernel, a batch with big tiles reports them
+    and the next decode runs the full one, and after 8 launches seen to run
+    without such tiles the lean one again -- counted on launches that ran,
+    so a burst of issued launches does not flip it back (each launch here is
+    synchronised, as the slowest case).  Outputs checked against the oracle
+    throughout."""
     import qhuff
     if os.environ.get("QHUFF_KERNELS"):
         pytest.skip("QHUFF_KERNELS pins the variant")
@@ -464,10 +466,10 @@ def test_kernel_variant_switch():
         E, D = qhuff.KIND_ENCODE, qhuff.KIND_DECODE
         check_encode(c, sdata, soff, 0)
         check_decode(c, sh, sho)
-        assert (c.kernel_variant(E), c.kernel_variant(D)) == (0, 0)
-        check_encode(c, bdata, boff, 0)          # lean; reports big tiles
-        check_decode(c, bh, bho)
-        assert (c.kernel_variant(E), c.kernel_variant(D)) == (0, 0)
+        assert (c.kernel_variant(E), c.kernel_variant(D)) == (1, 0)
+        check_encode(c, bdata, boff, 0)
+        check_decode(c, bh, bho)                 # lean; reports big tiles
+        assert (c.kernel_variant(E), c.kernel_variant(D)) == (1, 0)
         check_encode(c, bdata, boff, 0)
         check_decode(c, bh, bho)
         assert (c.kernel_variant(E), c.kernel_variant(D)) == (1, 1)
@@ -476,7 +478,10 @@ def test_kernel_variant_switch():
             check_encode(c, sdata, soff, 0)
             check_decode(c, sh, sho)
             seen.append((c.kernel_variant(E), c.kernel_variant(D)))
-        assert seen[0] == (1, 1) and seen[-1] == (0, 0), seen
+        assert seen[0] == (1, 1) and seen[-1] == (1, 0), seen
+        c.batch_hint(E, 0)                       # a hint still picks lean
+        check_encode(c, sdata, soff, 0)
+        assert c.kernel_variant(E) == 0
     finally:
         c.close()
 
