@@ -448,6 +448,34 @@ dense_or(QH_LDS uint32_t *dense, uint32_t pos, uint32_t v, uint32_t len)
                           __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// dense pass: a lane's 4-byte groups in pairs, one 64-bit value and three
+// ORs per pair instead of two per group (encode lab: dense pass 5.27k ->
+// 4.46k cycles per tile at 12 waves/CU; kernel 0.990 of the per-group ORs
+// in 3 same-box pairs, corpus encode 0.976, profiles/r05_dp; skipping the
+// third OR where it is zero: 4.67k, 0.994)
+#ifndef QH_DENSE_PAIR
+#define QH_DENSE_PAIR 1
+#endif
+
+// OR the right-aligned len-bit value v (len <= 64) into the dense stream at
+// bit pos: three words (past the stream: its last three)
+__device__ __forceinline__ void
+dense_or64(QH_LDS uint32_t *dense, uint32_t pos, uint64_t v, uint32_t len)
+{
+    const uint64_t x = v << ((64u - len) & 63);
+    const uint32_t sh = pos & 31;
+    const uint32_t w = min(pos >> 5, (uint32_t) kDenseWords - 3);
+    const uint32_t w0 = (uint32_t) (x >> (32 + sh));
+    const uint32_t w1 = (uint32_t) (x >> sh);
+    const uint32_t w2 = sh ? (uint32_t) (x << (32 - sh)) : 0u;
+    __hip_atomic_fetch_or(&dense[w], w0, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(&dense[w + 1], w1, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(&dense[w + 2], w2, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Byte-parallel pass over the tile's staged chunks (lane l holds span chunks
 // l, l + 64, l + 128): code lengths per byte (u8, into the out stage), the
 // dense offset of every chunk (s0) and the codes of all span bytes back to
@@ -509,6 +537,33 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
         lens4[c] = (u32x4){lp[0], lp[1], lp[2], lp[3]};
         wv->s0[c] = p0;
         uint32_t pos = p0;
+#if QH_DENSE_PAIR
+        // groups in pairs: one 64-bit value, three ORs instead of four
+        if (!__builtin_amdgcn_ballot_w64((G[0] > 32) | (G[1] > 32) | (G[2] > 32)
+                                         | (G[3] > 32)))
+        {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+            {
+                uint32_t v[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e)
+                {
+                    const int g = 2 * h + e;
+                    uint32_t x = m[4 * g] & 0x7ffffffu;
+#pragma unroll
+                    for (int j = 1; j < 4; ++j)
+                        x = (x << (m[4 * g + j] >> 27)) | (m[4 * g + j] & 0x7ffffffu);
+                    v[e] = x;
+                }
+                const uint32_t n = G[2 * h] + G[2 * h + 1];
+                dense_or64(wv->dense, pos, ((uint64_t) v[0] << G[2 * h + 1]) | v[1],
+                           n);
+                pos += n;
+            }
+            continue;
+        }
+#endif
 #pragma unroll
         for (int g = 0; g < 4; ++g)
         {

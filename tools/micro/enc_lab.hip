@@ -246,6 +246,21 @@ enc_lab(EncArgs a, int reps, MbOut *res)
         for (int r = 0; r < 12; ++r)
             ref[r] = 64 * r + lane < nw ? wv->out[64 * r + lane] : 0u;
         wave_sync();
+        // the dense stream against the bit packer on the staged input
+        {
+            QH_LDS u32x4 *o4 = (QH_LDS u32x4 *) wv->out;
+            for (uint32_t i = lane; i < (total + 15) / 16 + 1; i += 64)
+                o4[i] = (u32x4){0, 0, 0, 0};
+            wave_sync();
+            if (sz)
+                emit_bits(wv->in, pol.rs, pol.re, pol.mode, pol.z.huff, pol.z.plen,
+                          sm->enc, wv->out, incl - sz);
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 12; ++r)
+                bad += 64 * r + lane < nw && wv->out[64 * r + lane] != ref[r];
+            wave_sync();
+        }
         if (pol.dense)
             emit_words(wv, kWT, incl - sz, sz, pol.ds, pol.bits, total);
         wave_sync();
