@@ -468,6 +468,15 @@ dense_or64(QH_LDS uint32_t *dense, uint32_t pos, uint64_t v, uint32_t len)
     const uint32_t w0 = (uint32_t) (x >> (32 + sh));
     const uint32_t w1 = (uint32_t) (x >> sh);
     const uint32_t w2 = sh ? (uint32_t) (x << (32 - sh)) : 0u;
+#ifdef QH_TIME_DENSE_STORE                   // timing builds only: wrong output
+    if (QH_TIME_DENSE_STORE == 1)
+    {
+        dense[w] = w0;
+        dense[w + 1] = w1;
+        dense[w + 2] = w2;
+    }
+    return;
+#endif
     __hip_atomic_fetch_or(&dense[w], w0, __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_WORKGROUP);
     __hip_atomic_fetch_or(&dense[w + 1], w1, __ATOMIC_RELAXED,
