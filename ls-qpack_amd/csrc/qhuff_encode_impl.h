@@ -50,7 +50,7 @@ struct EncSmem
 {
     static constexpr bool kMtRep = QH_MT_REP;
     u32x2 enc[257];
-    uint32_t mt[256];                // dense pass: code[26:0] | len << 27
+    uint32_t mt[256];                // dense pass: mt_entry(code, len)
     uint32_t mtr[kMtRep ? 256 * 32 : 1];   // mt, 32 copies: [byte][copy]
     uint8_t len[256];
     EncWave w[kWaves];
@@ -448,6 +448,43 @@ dense_or(QH_LDS uint32_t *dense, uint32_t pos, uint32_t v, uint32_t len)
                           __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// QH_MT_LOW 1: the dense pass's table entry is code[26:0] << 5 | len (len
+// in the low bits: a group's four lengths gathered by two byte permutes,
+// and a shift takes the entry itself as its amount); 0: len << 27 | code.
+// Encode lab: dense pass 4.49k -> 3.99k cycles per tile at 12 waves/CU;
+// kernel 0.973 in 3 same-box pairs, corpus encode 0.978 (profiles/r05_low)
+#ifndef QH_MT_LOW
+#define QH_MT_LOW 1
+#endif
+__device__ __forceinline__ uint32_t
+mt_entry(uint32_t code, uint32_t len)
+{
+    return QH_MT_LOW ? ((code & 0x7ffffffu) << 5) | len
+                     : (code & 0x7ffffffu) | (len << 27);
+}
+__device__ __forceinline__ uint32_t
+mt_code(uint32_t m)
+{
+    return QH_MT_LOW ? m >> 5 : m & 0x7ffffffu;
+}
+__device__ __forceinline__ uint32_t
+mt_len(uint32_t m)
+{
+    return QH_MT_LOW ? m & 31u : m >> 27;
+}
+// the four lengths of entries a..d as bytes
+__device__ __forceinline__ uint32_t
+mt_lens4(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+#if QH_MT_LOW
+    const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0c0c0400u);
+    const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x04000c0cu);
+    return (lo | hi) & 0x1f1f1f1fu;
+#else
+    return (a >> 27) | ((b >> 27) << 8) | ((c >> 27) << 16) | ((d >> 27) << 24);
+#endif
+}
+
 // dense pass: a lane's 4-byte groups in pairs, one 64-bit value and three
 // ORs per pair instead of two per group (encode lab: dense pass 5.27k ->
 // 4.46k cycles per tile at 12 waves/CU; kernel 0.990 of the per-group ORs
@@ -534,8 +571,7 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
 #pragma unroll
         for (int g = 0; g < 4; ++g)
         {
-            lp[g] = (m[4 * g] >> 27) | ((m[4 * g + 1] >> 27) << 8)
-                  | ((m[4 * g + 2] >> 27) << 16) | ((m[4 * g + 3] >> 27) << 24);
+            lp[g] = mt_lens4(m[4 * g], m[4 * g + 1], m[4 * g + 2], m[4 * g + 3]);
             G[g] = __builtin_amdgcn_sad_u8(lp[g], 0u, 0u);
         }
         const uint32_t T = G[0] + G[1] + G[2] + G[3];
@@ -559,10 +595,11 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
                 for (int e = 0; e < 2; ++e)
                 {
                     const int g = 2 * h + e;
-                    uint32_t x = m[4 * g] & 0x7ffffffu;
+                    uint32_t x = mt_code(m[4 * g]);
 #pragma unroll
                     for (int j = 1; j < 4; ++j)
-                        x = (x << (m[4 * g + j] >> 27)) | (m[4 * g + j] & 0x7ffffffu);
+                        x = (x << (QH_MT_LOW ? m[4 * g + j] & 31u : mt_len(m[4 * g + j])))
+                          | mt_code(m[4 * g + j]);
                     v[e] = x;
                 }
                 const uint32_t n = G[2 * h] + G[2 * h + 1];
@@ -580,8 +617,8 @@ dense_pass(uint32_t n16, const QH_LDS uint32_t *mt, QH_LDS EncWave *wv)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
             {
-                cd[j] = m[4 * g + j] & 0x7ffffffu;
-                L[j] = m[4 * g + j] >> 27;
+                cd[j] = mt_code(m[4 * g + j]);
+                L[j] = mt_len(m[4 * g + j]);
             }
             if (__builtin_amdgcn_ballot_w64(G[g] > 32))
             {
@@ -1150,7 +1187,7 @@ enc_tables_load(QH_LDS SM *sm, const uint2 *enc_g, int tid)
             sm->len[tid] = (uint8_t) e.y;
             // (codes of 28 and 30 bits keep their low 27: the bits above
             // are ones, dense_pass puts them back)
-            const uint32_t m = (e.x & 0x7ffffffu) | (e.y << 27);
+            const uint32_t m = mt_entry(e.x, e.y);
             sm->mt[tid] = m;
             if constexpr (SM::kMtRep)
             {
