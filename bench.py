@@ -345,6 +345,12 @@ def main():
     else:
         kname, kms, alg = "qhuff_encode_kernel", enc_ms, alg_enc
     achieved = alg / (kms * 1e-3) / 1e9
+    # SURVEY 8(d)'s per-string figure counts separate in_len / out_len arrays
+    # (16 B / 17 B per string for encode / decode); this ABI derives lengths
+    # from the offsets (8 / 9 B).  Both fractions are reported.
+    alg_survey = (huff_bytes + raw_bytes + 17 * n
+                  if kname == "qhuff_decode_kernel"
+                  else raw_bytes + huff_bytes + 16 * n)
     traffic = None
     pmc_src = None
     if os.path.exists(args.pmc):
@@ -359,6 +365,9 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "frac_survey": round(alg_survey / (kms * 1e-3) / 1e9
+                                 / HBM_PEAK_GBS, 4),
+            "alg_bytes_survey": alg_survey,
             "kernel": kname, "kernel_us": round(kms * 1e3, 2),
             "alg_bytes": alg,
             "timing": "mean over %d %s launches of the timed region (every "
@@ -722,8 +731,11 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
 
 
 def run_config4(args, np, torch, qhuff):
-    """Config 4: one batch of --n4 strings over G GPUs of one process."""
-    import threading
+    """Config 4: one batch of --n4 strings over G GPUs of one process,
+    through the C-ABI's multi-context entry (include/qhuff.h
+    qhuff_encode_batch_multi / qhuff_decode_batch_multi: one host thread per
+    context inside the library, every shard's out_off rebased on its device
+    to the stitched batch's offsets)."""
     G = args.gpus
     # one device per shard; more shards than visible GPUs (a rehearsal on a
     # small box) share them round-robin
@@ -735,91 +747,75 @@ def run_config4(args, np, torch, qhuff):
     cuts = qhuff.shard_cuts(off, G)
     from qhuff import shard as S
     copies = max(1, min(args.copies, 2))
-    barrier = threading.Barrier(G)
-    res = [None] * G
-    errs = []
+    codecs, enc_sh, dec_sh, info = [], [[] for _ in range(copies)], \
+        [[] for _ in range(copies)], []
+    for g in range(G):
+        dev = torch.device("cuda", g % ndev)
+        torch.cuda.set_device(dev)
+        sd, soff, _ = S.shard_view(data, off, cuts, g)
+        n = len(soff) - 1
+        raw = int(soff[-1])
+        codec = qhuff.Codec(g % ndev)
+        codecs.append(codec)
+        st = torch.cuda.Stream(device=dev)
+        d_in = torch.from_numpy(np.ascontiguousarray(sd)).to(dev)
+        d_off = torch.from_numpy(soff.view(np.int32)).to(dev)
+        ecap = qhuff.encode_bound(raw, n, 0)
+        # decode input: this shard's Huffman payloads (shard-local offsets)
+        h_out, h_off = codec.encode(d_in, d_off, 0)
+        torch.cuda.synchronize(dev)
+        hb = int(h_off[-1].item())
+        dcap = qhuff.decode_bound(hb, n)
+        for k in range(copies):
+            enc_sh[k].append(dict(
+                in_=d_in if k == 0 else d_in.clone(),
+                in_off=d_off if k == 0 else d_off.clone(), n=n,
+                out=torch.empty(ecap, dtype=torch.uint8, device=dev),
+                out_off=torch.empty(n + 1, dtype=torch.int32, device=dev),
+                stream=st))
+            dec_sh[k].append(dict(
+                in_=h_out[:hb].clone(), in_off=h_off.clone(), n=n,
+                out=torch.empty(dcap, dtype=torch.uint8, device=dev),
+                out_off=torch.empty(n + 1, dtype=torch.int32, device=dev),
+                status=torch.empty(max(n, 1), dtype=torch.uint8, device=dev),
+                stream=st))
+        info.append({"n": n, "raw": raw, "huff": hb, "device": g % ndev})
+        del h_out
+    for g in range(G):
+        torch.cuda.synchronize(g % ndev)
 
-    def worker(g):
-        try:
-            torch.cuda.set_device(g % ndev)
-            dev = torch.device("cuda", g % ndev)
-            sd, soff, _ = S.shard_view(data, off, cuts, g)
-            n = len(soff) - 1
-            raw = int(soff[-1])
-            codec = qhuff.Codec(g % ndev)
-            st = torch.cuda.Stream(device=dev)
-            with torch.cuda.stream(st):
-                d_in = [torch.from_numpy(np.ascontiguousarray(sd)).to(dev)
-                        for _ in range(copies)]
-                d_off = [torch.from_numpy(soff.view(np.int32)).to(dev)
-                         for _ in range(copies)]
-                ecap = qhuff.encode_bound(raw, n, 0)
-                e_out = [torch.empty(ecap, dtype=torch.uint8, device=dev)
-                         for _ in range(copies)]
-                e_off = [torch.empty(n + 1, dtype=torch.int32, device=dev)
-                         for _ in range(copies)]
-                # decode input: this shard's Huffman payloads, made once
-                codec.encode_into(d_in[0], d_off[0], n, 0, e_out[0], e_off[0],
-                                  st)
-                st.synchronize()
-                hb = int(e_off[0][-1].item())
-                h_in = [e_out[0][:hb].clone() for _ in range(copies)]
-                h_off = [e_off[0].clone() for _ in range(copies)]
-                dcap = qhuff.decode_bound(hb, n)
-                o_out = [torch.empty(dcap, dtype=torch.uint8, device=dev)
-                         for _ in range(copies)]
-                o_off = [torch.empty(n + 1, dtype=torch.int32, device=dev)
-                         for _ in range(copies)]
-                o_st = [torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
-                        for _ in range(copies)]
-            st.synchronize()
+    def step(i):
+        k = i % copies
+        eb = qhuff.batch_multi(codecs, enc_sh[k], True, 0, rebase=True)
+        db = qhuff.batch_multi(codecs, dec_sh[k], False, rebase=True)
+        return eb, db
 
-            def step(i):
-                k = i % copies
-                codec.encode_into(d_in[k], d_off[k], n, 0, e_out[k], e_off[k],
-                                  st)
-                codec.decode_into(h_in[k], h_off[k], n, o_out[k], o_off[k],
-                                  o_st[k], st)
-
-            for i in range(args.warmup):
-                step(i)
-            st.synchronize()
-            barrier.wait()
-            st.synchronize()
-            t0 = time.perf_counter()
-            for i in range(args.steps):
-                step(args.warmup + i)
-            st.synchronize()
-            t1 = time.perf_counter()
-            barrier.wait()
-            k = (args.warmup + args.steps - 1) % copies
-            eo = e_off[k].cpu().numpy().view(np.uint32).copy()
-            res[g] = {"wall": t1 - t0, "n": n, "raw": raw, "huff": hb,
-                      "enc": (e_out[k][:int(eo[-1])].cpu().numpy(), eo),
-                      "dec": (o_out[k][:raw].cpu().numpy(),
-                              o_off[k].cpu().numpy().view(np.uint32).copy()),
-                      "status_ok": bool((o_st[k][:n] == 0).all().item()),
-                      "device_error": codec.device_error()}
-            codec.close()
-        except BaseException as e:          # surface in the main thread
-            errs.append((g, repr(e)))
-            barrier.abort()
-
-    ths = [threading.Thread(target=worker, args=(g,)) for g in range(G)]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    if errs:
-        sys.exit("config4 worker failed: %r" % errs)
-
-    wall = max(r["wall"] for r in res)
+    for i in range(args.warmup):
+        step(i)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        eb, db = step(args.warmup + i)
+    wall = time.perf_counter() - t0       # (the calls are synchronous)
     raw_total = int(off[-1])
     value = 2 * raw_total * args.steps / wall / 1e9
 
-    # stitched output == one pass over the whole batch on GPU 0
-    enc_m, enc_moff = S.merge([r["enc"] for r in res])
-    dec_m, dec_moff = S.merge([r["dec"] for r in res])
+    # stitched output (the last step's) == one pass over the whole batch on
+    # GPU 0; its decode == the input
+    k = (args.warmup + args.steps - 1) % copies
+    cat = lambda parts: np.concatenate(parts) if parts else np.zeros(0)
+    enc_m = cat([s["out"][:eb[g + 1] - eb[g]].cpu().numpy()
+                 for g, s in enumerate(enc_sh[k])])
+    enc_moff = cat([s["out_off"].cpu().numpy().view(np.uint32)[:-1]
+                    for s in enc_sh[k]] + [np.array([eb[-1]], np.uint32)])
+    dec_m = cat([s["out"][:db[g + 1] - db[g]].cpu().numpy()
+                 for g, s in enumerate(dec_sh[k])])
+    dec_moff = cat([s["out_off"].cpu().numpy().view(np.uint32)[:-1]
+                    for s in dec_sh[k]] + [np.array([db[-1]], np.uint32)])
+    status_ok = all(not s["status"][:s["n"]].cpu().numpy().any()
+                    for s in dec_sh[k])
+    dev_err = max(c.device_error() for c in codecs)
+    for c in codecs:
+        c.close()
     torch.cuda.set_device(0)
     c0 = qhuff.Codec(0)
     d_all = torch.from_numpy(data).cuda(0)
@@ -827,14 +823,13 @@ def run_config4(args, np, torch, qhuff):
     ref_out, ref_off = c0.encode(d_all, o_all, 0)
     torch.cuda.synchronize()
     ref_off = ref_off.cpu().numpy().view(np.uint32)
-    stitched_ok = (np.array_equal(enc_moff, ref_off) and np.array_equal(
-        enc_m, ref_out[:int(ref_off[-1])].cpu().numpy()))
-    roundtrip_ok = (np.array_equal(dec_moff, off)
-                    and np.array_equal(dec_m, data)
-                    and all(r["status_ok"] for r in res))
+    stitched_ok = (np.array_equal(enc_moff.astype(np.uint32), ref_off)
+                   and np.array_equal(enc_m,
+                                      ref_out[:int(ref_off[-1])].cpu().numpy()))
+    roundtrip_ok = (np.array_equal(dec_moff.astype(np.uint32), off)
+                    and np.array_equal(dec_m, data) and status_ok)
     c0.close()
-    dev_err = max(r["device_error"] for r in res)
-    shard_bytes = [r["raw"] for r in res]
+    shard_bytes = [r["raw"] for r in info]
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GB/s",
         "n_gpus": G, "steps": args.steps, "warmup": args.warmup,
@@ -845,16 +840,19 @@ def run_config4(args, np, torch, qhuff):
                 % args.alphabet,
         "config": {"workload": "config4", "strings": N,
                    "raw_bytes": raw_total,
-                   "parallelism": "%d GPUs, one host thread + stream + "
-                                  "qhuff_ctx each, qhuff_shard_cuts "
-                                  "byte-balanced shards, no collective" % G,
-                   "shard_strings": [r["n"] for r in res],
+                   "parallelism": "%d GPUs through qhuff_encode_batch_multi / "
+                                  "qhuff_decode_batch_multi (one host thread "
+                                  "+ stream + qhuff_ctx per shard, "
+                                  "qhuff_shard_cuts byte-balanced shards, "
+                                  "offsets rebased on device, no "
+                                  "collective)" % G,
+                   "shard_strings": [r["n"] for r in info],
                    "shard_raw_bytes": shard_bytes,
+                   "shard_devices": [r["device"] for r in info],
                    "shard_byte_balance": round(max(shard_bytes)
                                                / max(1, min(shard_bytes)), 6)},
-        "per_gpu": [{"gpu": g, "device": g % ndev, "wall_ms": round(r["wall"] * 1e3, 3),
-                     "gbps": round(2 * r["raw"] * args.steps / r["wall"]
-                                   / 1e9, 3)} for g, r in enumerate(res)],
+        "step": "encode call (all shards, synchronous) + decode call (all "
+                "shards, synchronous)",
         "stitched_equals_single_pass": bool(stitched_ok),
         "roundtrip_ok": bool(roundtrip_ok), "device_error": dev_err,
     }

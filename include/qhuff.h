@@ -52,8 +52,12 @@ extern "C" {
  *   6  QHUFF_MAX_STRLEN: qhuff_scan_field_section rejects (QHUFF_EPROTO) a
  *      literal whose declared length exceeds it; qhuff_decode_literals_ex
  *      rejects a literal whose decoded length does; qhuff_batch_hint /
- *      qhuff_batch_needs_full (the kernel variant from the batch) */
-#define QHUFF_ABI_VERSION 6
+ *      qhuff_batch_needs_full (the kernel variant from the batch)
+ *   7  qhuff_dec_int (the pre-parse's integer decoder); qhuff_decode_
+ *      literals_ex applies max_len to a field line's name + value;
+ *      qhuff_encode_batch_host_multi / qhuff_decode_batch_host_multi (one
+ *      batch over several contexts / GPUs) */
+#define QHUFF_ABI_VERSION 7
 
 /* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
 int qhuff_abi_version(void);
@@ -293,6 +297,16 @@ int qhuff_scan_encoder_stream(const uint8_t *buf, size_t len,
                               uint32_t max_lits, uint32_t *n_lits,
                               size_t *consumed);
 
+/* (ABI 7) The scanners' prefixed-integer decoder (RFC 7541 5.1) with the
+ * reference's rules: lsqpack_dec_int (lsqpack.c:2372-2437) given the whole
+ * integer in one buffer.  prefix_bits 1..8; the bits of buf[0] above the
+ * prefix are ignored.  QHUFF_OK with *value and *consumed (the integer's
+ * bytes), QHUFF_ETRUNC when buf ends inside the integer (the reference's -1),
+ * QHUFF_EPROTO when the value does not fit 64 bits or the integer runs past
+ * 10 continuation bytes (its -2). */
+int qhuff_dec_int(const uint8_t *buf, size_t len, unsigned prefix_bits,
+                  uint64_t *value, size_t *consumed);
+
 /* Output bytes qhuff_decode_literals_host may write for these literals. */
 uint64_t qhuff_literals_bound(const struct qhuff_literal *lits, uint32_t n);
 
@@ -436,6 +450,54 @@ int qhuff_batch_needs_full(const uint32_t *in_off, uint32_t n);
  * (SURVEY.md section 8(e)). */
 int qhuff_shard_cuts(const uint32_t *in_off, uint32_t n, uint32_t g,
                      uint32_t *cuts);
+
+/* (ABI 7) One batch over g contexts -- one per GPU, or several on one GPU
+ * (distinct contexts; none in use by another thread during the call).  The
+ * path shards trivially (a string's output depends only on its own bytes,
+ * lsqpack.c:5085-5195, 5234-5466): the batch is cut by qhuff_shard_cuts
+ * into g contiguous shards, shard k runs on ctxs[k] on a host thread of its
+ * own (the calling thread takes shard 0), and the outputs are stitched by
+ * each shard's base, the exclusive scan of the shard totals.  No
+ * collective.
+ *
+ * Host memory: the arguments, outputs and return codes of
+ * qhuff_encode_batch_host / qhuff_decode_batch_host on one context, and the
+ * same bytes (out_off is global).  Each shard's uploads, kernels and
+ * downloads run unsynchronised; only its copies into `out` wait for the
+ * earlier shards' totals.  Synchronous. */
+int qhuff_encode_batch_host_multi(qhuff_ctx *const *ctxs, uint32_t g,
+                                  const uint8_t *in, const uint32_t *in_off,
+                                  uint32_t n, unsigned mode, uint8_t *out,
+                                  uint32_t *out_off);
+int qhuff_decode_batch_host_multi(qhuff_ctx *const *ctxs, uint32_t g,
+                                  const uint8_t *in, const uint32_t *in_off,
+                                  uint32_t n, uint8_t *out, uint32_t *out_off,
+                                  uint8_t *status);
+
+/* Device-resident shards (shard k in ctxs[k]'s device memory, laid out as
+ * for qhuff_encode_batch / qhuff_decode_batch; status unused by encode;
+ * stream: an opaque hipStream_t of that device, NULL = its default stream).
+ * Launches every shard, waits for them, and writes base[0 .. g]: base[k] =
+ * the output bytes of shards [0, k), base[g] the total.  rebase != 0: shard
+ * k's out_off (n_k + 1 entries) is also rebased by base[k] on its device, so
+ * that it indexes the concatenation of the shards' outputs (the stitched
+ * batch; the total must fit 32 bits, else QHUFF_ERANGE).  Synchronous. */
+struct qhuff_shard
+{
+    const uint8_t  *in;
+    const uint32_t *in_off;
+    uint32_t        n;
+    uint8_t        *out;
+    uint32_t       *out_off;
+    uint8_t        *status;
+    void           *stream;
+};
+int qhuff_encode_batch_multi(qhuff_ctx *const *ctxs, uint32_t g,
+                             const struct qhuff_shard *shards, unsigned mode,
+                             uint64_t *base, int rebase);
+int qhuff_decode_batch_multi(qhuff_ctx *const *ctxs, uint32_t g,
+                             const struct qhuff_shard *shards, uint64_t *base,
+                             int rebase);
 
 /* Synthetic header-string batch: xorshift64
  * seeded with `seed` (0 -> 0x9E3779B97F4A7C15); len = min_len +

@@ -134,6 +134,63 @@ rc_of(int r)
 
 }  // namespace
 
+// Name lengths of the QPACK static table (RFC 9204 Appendix A; the
+// reference's static_table[], lsqpack.c:104-209 -- the list in
+// tests/golden/qpack_static_table.json, which test_frames.py checks this
+// against through qhuff_decode_literals_ex).
+static const uint8_t kStaticNameLen[99] = {
+    10, 5, 3, 19, 14, 6, 4, 4, 17, 13, 13, 4, 8, 7, 10, 7, 7, 7, 7, 7, 7, 7,
+    7, 7, 7, 7, 7, 7, 7, 6, 6, 15, 13, 28, 28, 27, 13, 13, 13, 13, 13, 13,
+    16, 16, 12, 12, 12, 12, 12, 12, 12, 12, 12, 12, 12, 5, 25, 25, 25, 4, 4,
+    22, 16, 7, 7, 7, 7, 7, 7, 7, 7, 7, 15, 32, 32, 28, 28, 28, 28, 29, 30,
+    29, 29, 7, 13, 23, 10, 9, 9, 8, 6, 7, 6, 19, 25, 10, 15, 15, 15};
+
+namespace qhuff {
+
+// The length of the name a field-section VALUE literal's instruction refers
+// to, when the framing alone knows it: a static name reference (01NT with
+// T = 1, 4-bit index; lsqpack.c:3620-3642 header_out_begin_static_nameref
+// copies static_table[idx].name into the header buffer) -> its length;
+// a dynamic or post-base reference (the dynamic table stays with the
+// reference) or anything else -> 0.  buf: the buffer lits' offsets are
+// relative to (the instruction lies in [l.instr, l.pos - l.hdr_len)).
+uint32_t
+field_ref_name_len(const uint8_t *buf, const struct qhuff_literal &l)
+{
+    if (l.kind != QHUFF_LIT_VALUE || l.hdr_len > l.pos
+            || (uint64_t) l.instr + 1 > l.pos - l.hdr_len)
+        return 0;
+    const uint8_t *p = buf + l.instr, *const end = buf + (l.pos - l.hdr_len);
+    if ((*p & 0xd0) != 0x50)                 // 01NT, T = 1
+        return 0;
+    uint32_t idx;
+    if (dec_int24(&p, end, 4, &idx) || idx >= sizeof(kStaticNameLen))
+        return 0;
+    return kStaticNameLen[idx];
+}
+
+}  // namespace qhuff
+
+// (ABI 7) the scanners' integer decoder on its own: lsqpack_dec_int
+// (lsqpack.c:2372-2437) on a complete buffer -- pinned to the reference's
+// own vectors (test/test_int.c:19-183, tests/golden/kat_int.json)
+extern "C" int
+qhuff_dec_int(const uint8_t *buf, size_t len, unsigned prefix_bits,
+              uint64_t *value, size_t *consumed)
+{
+    if ((!buf && len) || !value || !consumed || prefix_bits < 1
+            || prefix_bits > 8)
+        return QHUFF_EINVAL;
+    const uint8_t *p = buf;
+    uint64_t v = 0;
+    const int r = dec_int(&p, buf + len, prefix_bits, &v);
+    if (r)
+        return rc_of(r);
+    *value = v;
+    *consumed = (size_t) (p - buf);
+    return QHUFF_OK;
+}
+
 extern "C" int
 qhuff_scan_field_section(const uint8_t *buf, size_t len, uint32_t pos_base,
                          struct qhuff_literal *lits, uint32_t max_lits,

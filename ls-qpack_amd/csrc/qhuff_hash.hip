@@ -270,6 +270,45 @@ launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st,
     return hipGetLastError();
 }
 
+// Shard stitching (qhuff_*_batch_multi): off[i] += add for i in [0, n],
+// four offsets per lane with 16-byte accesses where the array allows
+// (a grid-stride loop: every wave exits when its range is done).
+__global__ __launch_bounds__(256) void
+qhuff_rebase_kernel(uint32_t *off, uint64_t n, uint32_t add)
+{
+    const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+    const uint64_t head = (4 - (((uintptr_t) off >> 2) & 3)) & 3;   // to 16 B
+    const uint64_t h = head < n ? head : n;
+    const uint64_t t = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < h)
+        off[t] += add;
+    U4 *v = (U4 *) (off + h);
+    const uint64_t nv = (n - h) / 4;
+    for (uint64_t i = t; i < nv; i += stride)
+    {
+        u32x4 x = v[i].v;
+        x.x += add;
+        x.y += add;
+        x.z += add;
+        x.w += add;
+        v[i].v = x;
+    }
+    for (uint64_t i = h + 4 * nv + t; i < n; i += stride)
+        off[i] += add;
+}
+
+hipError_t
+launch_rebase(uint32_t *off, uint64_t n, uint32_t add, hipStream_t st)
+{
+    if (n == 0 || add == 0)
+        return hipSuccess;
+    const uint64_t need = (n / 4 + 255) / 256 + 1;
+    const uint32_t grid = (uint32_t) (need < 2048 ? need : 2048);
+    hipLaunchKernelGGL(qhuff_rebase_kernel, dim3(grid), dim3(256), 0, st, off,
+                       n, add);
+    return hipGetLastError();
+}
+
 int
 hash_waves_per_block()
 {

@@ -25,6 +25,11 @@
 
 using namespace qhuff;
 
+namespace qhuff {
+// qhuff_frames.cpp: a VALUE literal's static-table name length, or 0
+uint32_t field_ref_name_len(const uint8_t *buf, const struct qhuff_literal &l);
+}
+
 struct DevTables
 {
     uint32_t win[kWinSize];              // 16-byte aligned (copied as uint4)
@@ -252,10 +257,16 @@ fail(qhuff_ctx *c, hipError_t e, const char *what)
 // of any context and freed with the last context that used it.  So a
 // context's own device memory stays small (tables, look-back flags, its
 // staging), however many contexts a process opens.  Contexts order their
-// launches on the pool: while more than one context holds it, each launch
-// on it records the pool's event, and a launch of another context waits for
-// it first (a context's own launches are ordered by prepare_launch); a
-// context that joins a pool in use waits for the device once.
+// launches on the pool: each launch on it records the pool's event, and a
+// launch of another context waits for it first (a context's own launches
+// are ordered by prepare_launch).  So a context that joins a pool in use
+// orders its first launch after the last one on it with a stream wait --
+// no device synchronisation, which would also wait for other libraries'
+// streams and a resident service kernel, under the pool's lock (ADVICE
+// r05) -- and a pool outgrown by a larger grid is retired, not freed,
+// until its last user closes.  Launches of different contexts on the pool
+// are serialised this way even when they write no slot (INTEGRATION.md
+// section 6).
 constexpr uint32_t kSmallGrid = 8;
 constexpr uint64_t kWaveSlotBytes = (uint64_t) kBigSlots * kBigSlotBytes;
 constexpr int kMaxDevices = 64;
@@ -266,8 +277,9 @@ struct SlotPool
     uint8_t *p = nullptr;
     uint64_t waves = 0;                  // slots for this many waves
     int refs = 0;                        // contexts that used it
-    hipEvent_t ev = nullptr;             // the last launch on it (refs > 1)
+    hipEvent_t ev = nullptr;             // the last launch on it
     const qhuff_ctx *ev_ctx = nullptr;   // whose launch ev follows
+    std::vector<uint8_t *> retired;      // outgrown pools (freed with it)
 };
 static SlotPool g_pool[kMaxDevices];
 
@@ -282,6 +294,9 @@ pool_release(int device)
         return;
     if (sp.p)
         (void) hipFree(sp.p);
+    for (uint8_t *q : sp.retired)
+        (void) hipFree(q);
+    sp.retired.clear();
     if (sp.ev)
         (void) hipEventDestroy(sp.ev);
     sp.p = nullptr;
@@ -335,10 +350,6 @@ with_slots(qhuff_ctx *c, uint32_t grid, uint64_t wpb, bool *full,
     std::lock_guard<std::mutex> g(sp.mu);
     if (!c->pool_ref)
     {
-        // joining: another context's launches on the pool are not recorded
-        // while it was alone -- wait for them once
-        if (sp.refs > 0)
-            HIPCHK(c, hipDeviceSynchronize());
         ++sp.refs;
         c->pool_ref = true;
     }
@@ -347,9 +358,9 @@ with_slots(qhuff_ctx *c, uint32_t grid, uint64_t wpb, bool *full,
     {
         if (sp.p)
         {
-            // (a grid larger than any seen: every user idle first)
-            HIPCHK(c, hipDeviceSynchronize());
-            (void) hipFree(sp.p);
+            // (a grid larger than any seen: launches still running on the
+            // old pool keep it until the pool's last user closes)
+            sp.retired.push_back(sp.p);
             sp.p = nullptr;
             sp.waves = 0;
         }
@@ -367,7 +378,7 @@ with_slots(qhuff_ctx *c, uint32_t grid, uint64_t wpb, bool *full,
     if (sp.ev && sp.ev_ctx && sp.ev_ctx != c)
         HIPCHK(c, hipStreamWaitEvent(st, sp.ev, 0));
     const int rc = launch(sp.p);
-    if (rc == QHUFF_OK && sp.refs > 1)
+    if (rc == QHUFF_OK)
     {
         if (!sp.ev)
             HIPCHK(c, hipEventCreateWithFlags(&sp.ev, hipEventDisableTiming));
@@ -852,15 +863,15 @@ static bool
 pick_full(qhuff_ctx *c, int kind, Coord *k)
 {
     k->rare = c->rare_dev + 2 * kind;
+    // a hint applies to the next launch of its kind only, whatever decides
+    // this one
+    const int hint = c->hint[kind];
+    c->hint[kind] = -1;
     if (c->kernels)
         return c->last_full[kind] = c->kernels == 2;
-    if (c->hint[kind] >= 0)
-    {
+    if (hint >= 0)
         // the host path read this batch's offsets (host_hint): no history
-        const bool f = c->hint[kind] > 0;
-        c->hint[kind] = -1;
-        return c->last_full[kind] = f;
-    }
+        return c->last_full[kind] = hint > 0;
     if (!kHistory[kind])
         return c->last_full[kind] = true;
     volatile uint32_t *r = c->rare_host + 2 * kind;
@@ -976,6 +987,8 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     bool full = false;
     if (!c->keep_rejected)
         full = pick_full(c, 1, &a.c);
+    else
+        c->hint[1] = -1;                 // (consumed by this launch too)
     rc = with_slots(c, grid, wpb, &full, st, [&](uint8_t *slots) -> int {
         a.c.big = slots;
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1181,10 +1194,54 @@ qhuff_batch_needs_full(const uint32_t *off, uint32_t n)
 // Stage layout (pinned and device alike): [in bytes | in_off (n + 1) |
 // out: per-chunk bound regions | out_off: n_i + 1 per chunk | status n].
 // The kernels read the original offsets: `in` is passed rebased by -in_off[0].
+//
+// Shard k of a multi-context call (qhuff_*_batch_host_multi, `sync`): the
+// shard's output goes to `out` at a base only known once every earlier shard
+// has sized its output, so its copies out of the pinned stage wait until
+// all its chunks are fetched and the base is published -- its uploads,
+// kernels and downloads never wait for another shard.
+struct ShardSync
+{
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint64_t> total;         // output bytes of each shard
+    std::vector<char> known;
+    bool failed = false;
+    explicit ShardSync(unsigned g) : total(g, 0), known(g, 0) {}
+    void publish(unsigned k, uint64_t t)
+    {
+        std::lock_guard<std::mutex> l(mu);
+        total[k] = t;
+        known[k] = 1;
+        cv.notify_all();
+    }
+    void fail()
+    {
+        std::lock_guard<std::mutex> l(mu);
+        failed = true;
+        cv.notify_all();
+    }
+    // the output bytes of shards [0, k), or ~0 if one of them failed
+    uint64_t base_of(unsigned k)
+    {
+        std::unique_lock<std::mutex> l(mu);
+        uint64_t b = 0;
+        for (unsigned j = 0; j < k; ++j)
+        {
+            cv.wait(l, [&] { return known[j] || failed; });
+            if (failed)
+                return ~0ull;
+            b += total[j];
+        }
+        return b;
+    }
+};
+
 static int
 host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
            uint32_t n, unsigned mode, uint8_t *out, uint32_t *out_off,
-           uint8_t *status)
+           uint8_t *status, ShardSync *sync = nullptr, unsigned shard = 0,
+           bool last_shard = true)
 {
     if (!c || !in_off || !out_off || (n && (!in || !out)) || (!enc && n && !status))
         return QHUFF_EINVAL;
@@ -1305,24 +1362,61 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
 
     if (n == 0)
     {
-        out_off[0] = 0;
+        if (sync)
+        {
+            sync->publish(shard, 0);
+            base = sync->base_of(shard);
+            if (base == ~0ull)
+                return QHUFF_EDEVICE;
+        }
+        if (last_shard)
+            out_off[0] = (uint32_t) base;
         return QHUFF_OK;
     }
-    for (unsigned i = 0; i < K; ++i)
+    if (sync)
     {
-        if ((rc = stage_in(i)))
+        // every chunk in flight first, then the copies out at the base
+        for (unsigned i = 0; i < K; ++i)
+        {
+            if ((rc = stage_in(i)))
+                return rc;
+            if (i >= 1 && (rc = fetch(i - 1)))
+                return rc;
+        }
+        if ((rc = fetch(K - 1)))
             return rc;
-        if (i >= 1 && (rc = fetch(i - 1)))
-            return rc;
-        if (i >= 2 && (rc = unstage(i - 2)))
-            return rc;
+        uint64_t t = 0;
+        for (unsigned i = 0; i < K; ++i)
+            t += tot[i];
+        sync->publish(shard, t);
+        base = sync->base_of(shard);
+        if (base == ~0ull)
+            return QHUFF_EDEVICE;
+        for (unsigned i = 0; i < K; ++i)
+            if ((rc = unstage(i)))
+                return rc;
     }
-    if ((rc = fetch(K - 1)))
-        return rc;
-    for (unsigned i = K >= 2 ? K - 2 : 0; i < K; ++i)
-        if ((rc = unstage(i)))
+    else
+    {
+        for (unsigned i = 0; i < K; ++i)
+        {
+            if ((rc = stage_in(i)))
+                return rc;
+            if (i >= 1 && (rc = fetch(i - 1)))
+                return rc;
+            if (i >= 2 && (rc = unstage(i - 2)))
+                return rc;
+        }
+        if ((rc = fetch(K - 1)))
             return rc;
-    out_off[n] = (uint32_t) base;
+        for (unsigned i = K >= 2 ? K - 2 : 0; i < K; ++i)
+            if ((rc = unstage(i)))
+                return rc;
+    }
+    // (a shard's closing offset is the next shard's first one: written by
+    // the last shard only)
+    if (last_shard)
+        out_off[n] = (uint32_t) base;
     {
         if ((rc = mirror_error(c)))
             return rc;
@@ -1359,6 +1453,183 @@ qhuff_decode_batch_host(qhuff_ctx *c, const uint8_t *in,
     if (c && c->svc)                      // (see qhuff_encode_batch_host)
         return svc_call(c->svc, false, in, in_off, n, 0, out, out_off, status);
     return host_batch(c, false, in, in_off, n, 0, out, out_off, status);
+}
+
+// ---- one batch over several contexts ---------------
+//
+// The path shards trivially -- a string's output depends on its own bytes
+// and the static table only (lsqpack.c:5085-5195, 5234-5466) -- so a batch
+// is cut by input bytes (qhuff_shard_cuts) into one contiguous shard per
+// context, every shard runs on its own host thread (the caller's thread
+// takes shard 0), and the outputs are stitched by adding each shard's base
+// (the exclusive scan of the shard totals) to its offsets.  No collective:
+// the only cross-shard dependency is that base.
+
+// contexts distinct and non-null
+static bool
+ctxs_ok(qhuff_ctx *const *ctxs, uint32_t g)
+{
+    if (!ctxs || g == 0 || g > 1024)
+        return false;
+    for (uint32_t k = 0; k < g; ++k)
+    {
+        if (!ctxs[k])
+            return false;
+        for (uint32_t j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k])
+                return false;
+    }
+    return true;
+}
+
+// run f(k) for k in [0, g): threads for k >= 1, the caller for k = 0;
+// the first failing return code (in shard order), or QHUFF_OK
+template <class F>
+static int
+run_shards(uint32_t g, F f)
+{
+    std::vector<int> rc(g, QHUFF_OK);
+    std::vector<std::thread> th;
+    th.reserve(g ? g - 1 : 0);
+    for (uint32_t k = 1; k < g; ++k)
+        th.emplace_back([&rc, &f, k] { rc[k] = f(k); });
+    rc[0] = f(0);
+    for (auto &t : th)
+        t.join();
+    for (uint32_t k = 0; k < g; ++k)
+        if (rc[k])
+            return rc[k];
+    return QHUFF_OK;
+}
+
+static int
+host_multi(qhuff_ctx *const *ctxs, uint32_t g, bool enc, const uint8_t *in,
+           const uint32_t *in_off, uint32_t n, unsigned mode, uint8_t *out,
+           uint32_t *out_off, uint8_t *status)
+{
+    if (!ctxs_ok(ctxs, g) || !in_off || !out_off || (n && (!in || !out))
+            || (!enc && n && !status))
+        return QHUFF_EINVAL;
+    if (enc && mode != 0 && mode != 3 && mode != 5 && mode != 7)
+        return QHUFF_EINVAL;
+    const uint64_t bytes = (uint64_t) in_off[n] - in_off[0];
+    if ((enc ? qhuff_encode_bound(bytes, n, mode) : qhuff_decode_bound(bytes, n))
+            > 0xffffffffull)
+        return QHUFF_ERANGE;
+    std::vector<uint32_t> cuts(g + 1);
+    int rc = qhuff_shard_cuts(in_off, n, g, cuts.data());
+    if (rc)
+        return rc;
+    ShardSync sync(g);
+    return run_shards(g, [&](uint32_t k) -> int {
+        const uint32_t s0 = cuts[k], m = cuts[k + 1] - s0;
+        const int r = host_batch(ctxs[k], enc, in, in_off + s0, m, mode, out,
+                                 out_off + s0, status ? status + s0 : nullptr,
+                                 &sync, k, k + 1 == g);
+        if (r)
+            sync.fail();
+        return r;
+    });
+}
+
+extern "C" int
+qhuff_encode_batch_host_multi(qhuff_ctx *const *ctxs, uint32_t g,
+                              const uint8_t *in, const uint32_t *in_off,
+                              uint32_t n, unsigned mode, uint8_t *out,
+                              uint32_t *out_off)
+{
+    return host_multi(ctxs, g, true, in, in_off, n, mode, out, out_off,
+                      nullptr);
+}
+
+extern "C" int
+qhuff_decode_batch_host_multi(qhuff_ctx *const *ctxs, uint32_t g,
+                              const uint8_t *in, const uint32_t *in_off,
+                              uint32_t n, uint8_t *out, uint32_t *out_off,
+                              uint8_t *status)
+{
+    return host_multi(ctxs, g, false, in, in_off, n, 0, out, out_off, status);
+}
+
+// Device-resident shards: shard k is already on ctxs[k]'s device.  Each
+// thread launches its shard and reads its total; the bases are the
+// exclusive scan; with rebase, a small kernel adds shard k's base to its
+// out_off on its own device (out_off then holds offsets into the
+// concatenation of the shards' outputs).  Synchronous.
+static int
+dev_multi(qhuff_ctx *const *ctxs, uint32_t g, bool enc,
+          const struct qhuff_shard *sh, unsigned mode, uint64_t *base,
+          int rebase)
+{
+    if (!ctxs_ok(ctxs, g) || !sh || !base)
+        return QHUFF_EINVAL;
+    ShardSync sync(g);
+    std::vector<uint64_t> bases(g + 1, 0);
+    const int rc = run_shards(g, [&](uint32_t k) -> int {
+        qhuff_ctx *c = ctxs[k];
+        const qhuff_shard &s = sh[k];
+        hipStream_t st = (hipStream_t) s.stream;
+        int r = enc ? qhuff_encode_batch(c, s.in, s.in_off, s.n, mode, s.out,
+                                         s.out_off, s.stream)
+                    : qhuff_decode_batch(c, s.in, s.in_off, s.n, s.out,
+                                         s.out_off, s.status, s.stream);
+        uint32_t t = 0;
+        if (!r)
+        {
+            hipError_t e = hipMemcpyAsync(&t, s.out_off + s.n, 4,
+                                          hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess)
+                e = hipStreamSynchronize(st);
+            if (e != hipSuccess)
+                r = fail(c, e, "shard total");
+        }
+        if (!r && c->err_host[0])
+            r = mirror_error(c);
+        if (r)
+        {
+            sync.fail();
+            return r;
+        }
+        sync.publish(k, t);
+        const uint64_t b = sync.base_of(k);
+        if (b == ~0ull)
+            return QHUFF_EDEVICE;
+        bases[k] = b;
+        if (b + t > 0xffffffffull)
+            return QHUFF_ERANGE;
+        if (rebase && b)
+        {
+            HIPCHK(c, hipSetDevice(c->device));
+            HIPCHK(c, launch_rebase(s.out_off, (uint64_t) s.n + 1,
+                                    (uint32_t) b, st));
+            HIPCHK(c, hipStreamSynchronize(st));
+        }
+        if (k + 1 == g)
+            bases[g] = b + t;
+        return QHUFF_OK;
+    });
+    if (rc)
+        return rc;
+    memcpy(base, bases.data(), 8ull * (g + 1));
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_encode_batch_multi(qhuff_ctx *const *ctxs, uint32_t g,
+                         const struct qhuff_shard *shards, unsigned mode,
+                         uint64_t *base, int rebase)
+{
+    if (mode != 0 && mode != 3 && mode != 5 && mode != 7)
+        return QHUFF_EINVAL;
+    return dev_multi(ctxs, g, true, shards, mode, base, rebase);
+}
+
+extern "C" int
+qhuff_decode_batch_multi(qhuff_ctx *const *ctxs, uint32_t g,
+                         const struct qhuff_shard *shards, uint64_t *base,
+                         int rebase)
+{
+    return dev_multi(ctxs, g, false, shards, 0, base, rebase);
 }
 
 // ---- low-latency service (qhuff_service.hip) -----------------------------------
@@ -1885,9 +2156,14 @@ qhuff_decode_literals_ex(qhuff_ctx *c, const uint8_t *buf,
     }
     if (nh)
     {
-        if (!c->pipe_ready && (rc = pipe_setup(c)))
-            return rc;
-        host_hint(c, false, hoff, nh);
+        // the variant from this batch (auto mode only: a pinned variant
+        // needs neither the copy workers nor the scan)
+        if (c->kernels == 0)
+        {
+            if (!c->pipe_ready && (rc = pipe_setup(c)))
+                return rc;
+            host_hint(c, false, hoff, nh);
+        }
         HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, o_out,
                                  hipMemcpyHostToDevice, st));
         rc = qhuff_decode_batch(c, c->d_stage, (const uint32_t *) (c->d_stage
@@ -1924,30 +2200,47 @@ qhuff_decode_literals_ex(qhuff_ctx *c, const uint8_t *buf,
     const uint8_t *dst = c->h_stage + o_st;
     uint64_t o = 0;
     uint32_t k = 0;
+    // max_len (field sections): the reference decodes a field line's name
+    // and value into ONE header buffer, which never grows past
+    // LSXPACK_MAX_STRLEN (header_out_grow_buf, lsqpack.c:3346-3351; its
+    // size is a uint16 lsxpack_strlen_t): a name decoded here (NAME literal
+    // of the same instruction) or a static-table name (field_ref_name_len)
+    // counts against its value.  A dynamic-table name is not known to the
+    // framing: that value is checked alone.
+    uint32_t name_len = 0, name_instr = 0;
+    bool have_name = false;
     for (uint32_t i = 0; i < n; ++i)
     {
         out_off[i] = (uint32_t) o;
+        uint32_t len = lits[i].len;
+        uint8_t stv = QHUFF_DEC_OK;
+        const uint8_t *src = buf + lits[i].pos;
         if (lits[i].huffman)
         {
             const uint32_t a = doo[k], b = doo[k + 1];
+            stv = dst[k];
             ++k;
-            if (max_len && b - a > max_len)
-            {
-                status[i] = QHUFF_DEC_ERROR;
-                continue;
-            }
-            status[i] = dst[k - 1];
-            memcpy(out + o, c->h_stage + o_out + a, b - a);
-            o += b - a;
+            len = b - a;
+            src = c->h_stage + o_out + a;
         }
-        else if (max_len && lits[i].len > max_len)
-            status[i] = QHUFF_DEC_ERROR;
-        else
+        uint32_t lim_used = 0;
+        if (max_len && lits[i].kind == QHUFF_LIT_VALUE)
+            lim_used = have_name && name_instr == lits[i].instr
+                     ? name_len : field_ref_name_len(buf, lits[i]);
+        have_name = false;
+        if (max_len && (uint64_t) lim_used + len > max_len)
+            stv = QHUFF_DEC_ERROR;
+        status[i] = stv;
+        if (stv != QHUFF_DEC_OK)
+            continue;
+        if (lits[i].kind == QHUFF_LIT_NAME)
         {
-            status[i] = QHUFF_DEC_OK;
-            memcpy(out + o, buf + lits[i].pos, lits[i].len);
-            o += lits[i].len;
+            have_name = true;
+            name_len = len;
+            name_instr = lits[i].instr;
         }
+        memcpy(out + o, src, len);
+        o += len;
     }
     out_off[n] = (uint32_t) o;
     return QHUFF_OK;

@@ -158,6 +158,9 @@ hipError_t launch_decode(const DecArgs &a, uint32_t grid, hipStream_t st,
 hipError_t launch_hash(const HashArgs &a, uint32_t max_grid, hipStream_t st,
                        hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t hash_occupancy(int *blocks_per_cu);
+// off[0 .. n) += add (shard stitching, qhuff_*_batch_multi)
+hipError_t launch_rebase(uint32_t *off, uint64_t n, uint32_t add,
+                         hipStream_t st);
 int hash_waves_per_block();
 hipError_t encode_occupancy(int *blocks_per_cu);
 hipError_t decode_occupancy(int *blocks_per_cu);

@@ -37,6 +37,9 @@ EXPORTS = (
     "qhuff_svc_open", "qhuff_svc_close", "qhuff_svc_encode",
     "qhuff_svc_decode", "qhuff_svc_stats",
     "qhuff_timing_enable", "qhuff_timing_read", "qhuff_kernel_variant",
+    "qhuff_dec_int", "qhuff_encode_batch_host_multi",
+    "qhuff_decode_batch_host_multi", "qhuff_encode_batch_multi",
+    "qhuff_decode_batch_multi",
     # include/qhuff_lsqpack.h
     "qhuff_lsqpack_enc_enc_str", "qhuff_lsqpack_huff_decode",
     "qhuff_lsqpack_set_decode_full", "qhuff_lsqpack_set_device",
@@ -61,6 +64,14 @@ class Literal(C.Structure):
                 ("huffman", C.c_uint8), ("prefix_bits", C.c_uint8),
                 ("kind", C.c_uint8), ("hdr_len", C.c_uint8),
                 ("instr", C.c_uint32)]
+
+
+class Shard(C.Structure):
+    """struct qhuff_shard (include/qhuff.h): one device-resident shard"""
+    _fields_ = [("in_", C.c_void_p), ("in_off", C.c_void_p),
+                ("n", C.c_uint32), ("out", C.c_void_p),
+                ("out_off", C.c_void_p), ("status", C.c_void_p),
+                ("stream", C.c_void_p)]
 
 
 class DecodeRetval(C.Structure):
@@ -210,6 +221,23 @@ def lib():
         L.qhuff_frame_literal.argtypes = [C.c_uint, vp, C.c_size_t,
                                           C.c_char_p, C.c_uint, C.c_char_p,
                                           C.c_uint]
+        L.qhuff_dec_int.restype = C.c_int
+        L.qhuff_dec_int.argtypes = [C.c_char_p, C.c_size_t, C.c_uint,
+                                    C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_size_t)]
+        L.qhuff_encode_batch_host_multi.restype = C.c_int
+        L.qhuff_encode_batch_host_multi.argtypes = [vp, C.c_uint32, vp, u32p,
+                                                    C.c_uint32, C.c_uint, vp,
+                                                    u32p]
+        L.qhuff_decode_batch_host_multi.restype = C.c_int
+        L.qhuff_decode_batch_host_multi.argtypes = [vp, C.c_uint32, vp, u32p,
+                                                    C.c_uint32, vp, u32p, vp]
+        L.qhuff_encode_batch_multi.restype = C.c_int
+        L.qhuff_encode_batch_multi.argtypes = [vp, C.c_uint32, vp, C.c_uint,
+                                               vp, C.c_int]
+        L.qhuff_decode_batch_multi.restype = C.c_int
+        L.qhuff_decode_batch_multi.argtypes = [vp, C.c_uint32, vp, vp,
+                                               C.c_int]
         _lib = L
     return _lib
 
@@ -275,6 +303,15 @@ def scan_encoder_stream(buf, pos_base=0):
     return rc, lits, consumed.value
 
 
+def dec_int(buf, prefix_bits):
+    """qhuff_dec_int (the scanners' lsqpack_dec_int, complete buffer) ->
+    (rc, value, consumed)."""
+    v, used = C.c_uint64(), C.c_size_t()
+    rc = lib().qhuff_dec_int(bytes(buf), len(buf), prefix_bits, C.byref(v),
+                             C.byref(used))
+    return rc, (v.value if rc == OK else None), (used.value if rc == OK else 0)
+
+
 def frame_literal(prefix_bits, s, huff, first_byte=0, dst_len=1 << 16):
     """lsqpack_enc_enc_str framing of s given its precomputed Huffman
     payload (include/qhuff.h qhuff_frame_literal) -> bytes or -1."""
@@ -329,6 +366,76 @@ def lsqpack_set_decode_full(fn):
     lib().qhuff_lsqpack_set_decode_full(
         C.cast(cb, C.c_void_p) if cb is not None else None)
     return cb
+
+
+# ---- one batch over several contexts (qhuff_*_batch_*multi) ---------------
+
+def _ctx_array(codecs):
+    arr = (C.c_void_p * len(codecs))(*[c._ctx.value for c in codecs])
+    return arr
+
+
+def encode_host_multi(codecs, data, in_off, mode=ENC_PAYLOAD):
+    """qhuff_encode_batch_host_multi: host batch sharded over the contexts
+    -> (out bytes, global out_off)."""
+    import numpy as np
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
+    n = len(in_off) - 1
+    out = np.zeros(encode_bound(int(in_off[-1] - in_off[0]), n, mode),
+                   dtype=np.uint8)
+    out_off = np.zeros(n + 1, dtype=np.uint32)
+    rc = lib().qhuff_encode_batch_host_multi(
+        _ctx_array(codecs), len(codecs), _np_ptr(data), _np_ptr(in_off), n,
+        mode, _np_ptr(out), _np_ptr(out_off))
+    if rc:
+        raise QhuffError("qhuff_encode_batch_host_multi: %d" % rc)
+    return out[:out_off[-1]], out_off
+
+
+def decode_host_multi(codecs, data, in_off):
+    """qhuff_decode_batch_host_multi -> (out bytes, out_off, status)."""
+    import numpy as np
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    in_off = np.ascontiguousarray(in_off, dtype=np.uint32)
+    n = len(in_off) - 1
+    out = np.zeros(decode_bound(int(in_off[-1] - in_off[0]), n),
+                   dtype=np.uint8)
+    out_off = np.zeros(n + 1, dtype=np.uint32)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    rc = lib().qhuff_decode_batch_host_multi(
+        _ctx_array(codecs), len(codecs), _np_ptr(data), _np_ptr(in_off), n,
+        _np_ptr(out), _np_ptr(out_off), _np_ptr(status))
+    if rc:
+        raise QhuffError("qhuff_decode_batch_host_multi: %d" % rc)
+    return out[:out_off[-1]], out_off, status[:n]
+
+
+def batch_multi(codecs, shards, encode, mode=ENC_PAYLOAD, rebase=True):
+    """qhuff_encode_batch_multi / qhuff_decode_batch_multi over
+    device-resident shards: shards[k] = dict(in_, in_off, n, out, out_off,
+    status, stream) of torch tensors / ints (stream: a torch stream or
+    None) -> base list (g + 1 entries)."""
+    g = len(codecs)
+    arr = (Shard * g)()
+    for k, s in enumerate(shards):
+        st = s.get("stream")
+        arr[k] = Shard(s["in_"].data_ptr(), s["in_off"].data_ptr(), s["n"],
+                       s["out"].data_ptr(), s["out_off"].data_ptr(),
+                       s["status"].data_ptr() if s.get("status") is not None
+                       else None,
+                       st.cuda_stream if st is not None else None)
+    base = (C.c_uint64 * (g + 1))()
+    if encode:
+        rc = lib().qhuff_encode_batch_multi(_ctx_array(codecs), g, arr, mode,
+                                            base, int(rebase))
+    else:
+        rc = lib().qhuff_decode_batch_multi(_ctx_array(codecs), g, arr, base,
+                                            int(rebase))
+    if rc:
+        raise QhuffError("qhuff_%s_batch_multi: %d"
+                         % ("encode" if encode else "decode", rc))
+    return list(base)
 
 
 # ---- device codec ----------------------------------------------------------

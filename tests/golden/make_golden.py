@@ -15,6 +15,8 @@ Sources (all under /root/reference):
                              header-block bytes)
   test/test_header_alloc_clamp.c  the two over-long-length blocks main()
                              builds (LSXPACK_MAX_STRLEN clamp, LQRHS_ERROR)
+  test/test_int.c            tests[] (lsqpack_dec_int vectors, fed one byte
+                             per call) + test_overlong_integer_full_buffer
   lsqpack.c                  static_table[] (QPACK static table, data)
   fuzz/input/256.100.1/*     interop-encode output, -t 256 -s 100 -a 1
   test/qifs/*.qif            QIF corpora the streams above were encoded from
@@ -45,7 +47,7 @@ TOK = re.compile(r'''
   | (?P<comment>/\*.*?\*/|//[^\n]*|\#[^\n]*)
   | (?P<str>"(?:\\.|[^"\\])*")
   | (?P<chr>'(?:\\.|[^'\\])')
-  | (?P<num>0[xX][0-9a-fA-F]+[uUlL]*|\d+[uUlL]*)
+  | (?P<num>0[xX][0-9a-fA-F]+[uUlL]*|0[bB][01]+[uUlL]*|\d+[uUlL]*)
   | (?P<id>[A-Za-z_]\w*)
   | (?P<op>[{}()\[\],.=|+\-*&<>;~!?:/%^])
   | (?P<other>.)
@@ -188,6 +190,8 @@ def evaluate(toks):
             src.append(str(ln))
         elif k == "id" and v == "NULL":
             return None
+        elif k == "id" and v == "UINT64_MAX":
+            src.append(str((1 << 64) - 1))
         elif k == "id" and v == "sizeof":
             # sizeof("literal") -> len + 1
             assert parts[i + 1][1] == "(" and parts[i + 2][0] == "str"
@@ -354,6 +358,31 @@ def main():
         "max_strlen": 65535, "max_strlen_source": "lsxpack_header.h:12-13",
         "clamp_sites": "lsqpack.c:3682-3685, 3769-3772, 3350-3351",
         "cases": clamp_cases(f)}
+
+    f = os.path.join(REF, "test/test_int.c")
+    iv = []
+    for t in find_array(f, "tests"):
+        e = {"source": "%s:%d" % (rel(f), t["it_lineno"]),
+             "prefix_bits": t["it_prefix_bits"],
+             "encoded": as_bytes(t["it_encoded"])[:t["it_enc_sz"]].hex(),
+             "retval": t["it_dec_retval"]}
+        if "it_decoded" in t:
+            e["decoded"] = str(t["it_decoded"])     # (u64: JSON-safe)
+        iv.append(e)
+    text = open(f, encoding="latin-1").read()
+    fn = text.index("test_overlong_integer_full_buffer (void)")
+    ov = find_array(f, "encoded")
+    rv = re.search(r"lsqpack_dec_int\(&src, encoded \+ sizeof\(encoded\), (\d+),"
+                   r"[^;]*;\s*assert\(rv == (-?\d+)\)", text[fn:], re.S)
+    out["kat_int.json"] = {
+        "dec_int": iv,
+        "note": "tests[] are fed one byte per lsqpack_dec_int call: every "
+                "strict prefix returns -1, the last byte the retval "
+                "(test/test_int.c:198-214)",
+        "overlong_full_buffer": {
+            "source": "%s:%d" % (rel(f), text.count("\n", 0, fn) + 1),
+            "prefix_bits": int(rv.group(1)),
+            "encoded": as_bytes(ov).hex(), "retval": int(rv.group(2))}}
 
     f = os.path.join(REF, "lsqpack.c")
     st = []

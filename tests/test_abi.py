@@ -44,7 +44,7 @@ def test_library_has_gfx950_code_object():
 def test_header_is_plain_c():
     """The boundary headers must compile as C99 with no HIP/torch types."""
     src = "".join('#include "%s"\n' % h for h in qhuff.HEADERS) + \
-        "int main(void){return QHUFF_ABI_VERSION != 6;}\n"
+        "int main(void){return QHUFF_ABI_VERSION != 7;}\n"
     r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-x", "c",
                         "-fsyntax-only", "-"], input=src, text=True,
                        capture_output=True)
@@ -117,9 +117,9 @@ def test_abi_version_matches_header():
     needed); ABI 2 kept version 1's 5-argument qhuff_huff_decode beside
     qhuff_huff_decode_ex; ABI 3 adds the qhuff_svc_* service
     and keeps every earlier entry point"""
-    assert qhuff.lib().qhuff_abi_version() == 6
+    assert qhuff.lib().qhuff_abi_version() == 7
     src = open(os.path.join(ROOT, "include", "qhuff.h")).read()
-    assert "#define QHUFF_ABI_VERSION 6" in src
+    assert "#define QHUFF_ABI_VERSION 7" in src
     assert "qhuff_huff_decode(qhuff_ctx *ctx, const unsigned char *src, " \
            "int src_len,\n                  unsigned char *dst, int dst_len);" \
         in src

@@ -151,3 +151,72 @@ def test_two_contexts_concurrent_small(n):
         assert np.array_equal(do[:len(data)].cpu().numpy(), data)
     c1.close()
     c2.close()
+
+
+@pytest.mark.gpu
+def test_two_contexts_share_slot_pool_big_tiles():
+    """both contexts WRITE the device's shared big-tile slot
+    pool at once (qhuff_host.cpp with_slots).  The batch is the reference's
+    QIF corpora (tiles whose 1,461-byte values overflow the 3 KB stages)
+    with a 4 KB string every 5,000 strings, 400k strings (~2 grid rounds)
+    -- full kernels pinned, so every launch codes big tiles through the
+    pool; two contexts on two streams, several launches back to back.
+    Their launches are ordered by the pool's event: bit-exact against the
+    oracle, no device error."""
+    import os
+    import random
+    import torch
+    import qhuff
+    from qhuff import workload
+    here = os.path.dirname(os.path.abspath(__file__))
+    data, off = workload.corpus_batch(400_000,
+                                      os.path.join(here, "golden", "data"))
+    strs = [bytes(data[off[i]:off[i + 1]]) for i in range(len(off) - 1)]
+    rng = random.Random(5)
+    for i in range(0, len(strs), 5000):
+        strs[i] = bytes(rng.choice(b"abcdefghij-_/") for _ in range(4096))
+    data, off = workload.pack(strs)
+    n = len(off) - 1
+    h, ho = O.encode_batch(data, off, 0)
+    sh = workload.tile_shares(data, off, ho)
+    assert sh["decode_slow_tile_share"] > 0 and sh["encode_slow_tile_share"] > 0
+    old = os.environ.get("QHUFF_KERNELS")
+    os.environ["QHUFF_KERNELS"] = "full"
+    try:
+        c1, c2 = qhuff.Codec(0), qhuff.Codec(0)
+    finally:
+        if old is None:
+            del os.environ["QHUFF_KERNELS"]
+        else:
+            os.environ["QHUFF_KERNELS"] = old
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    d = _dev(data, torch)
+    o = _dev(off.view(np.int32), torch)
+    hd = _dev(h, torch)
+    hod = _dev(ho.view(np.int32), torch)
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(3):
+        for c, s in ((c1, s1), (c2, s2)):
+            eo = torch.empty(qhuff.encode_bound(len(data), n, 0),
+                             dtype=torch.uint8, device="cuda")
+            eoo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+            do = torch.empty(qhuff.decode_bound(len(h), n), dtype=torch.uint8,
+                             device="cuda")
+            doo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+            st = torch.empty(n, dtype=torch.uint8, device="cuda")
+            c.encode_into(d, o, n, 0, eo, eoo, s)
+            c.decode_into(hd, hod, n, do, doo, st, s)
+            outs.append((eo, eoo, do, doo, st))
+    torch.cuda.synchronize()
+    assert c1.device_error() == 0 and c2.device_error() == 0
+    assert c1.kernel_variant(qhuff.KIND_DECODE) == 1
+    for eo, eoo, do, doo, st in outs:
+        eoo = eoo.cpu().numpy().view(np.uint32)
+        assert np.array_equal(eoo, ho)
+        assert np.array_equal(eo[:int(eoo[-1])].cpu().numpy(), h)
+        assert np.array_equal(doo.cpu().numpy().view(np.uint32), off)
+        assert not st.cpu().numpy().any()
+        assert np.array_equal(do[:len(data)].cpu().numpy(), data)
+    c1.close()
+    c2.close()

@@ -152,6 +152,83 @@ def clamp_kat():
         return json.load(f)
 
 
+def int_kat():
+    with open(os.path.join(G, "kat_int.json")) as f:
+        return json.load(f)
+
+
+def _int_cases():
+    kat = int_kat()
+    cases = list(kat["dec_int"])
+    # (fed whole by the reference test, not byte by byte: its error comes
+    # at the 10th continuation byte, before the buffer's end)
+    cases.append(dict(kat["overlong_full_buffer"], whole=True))
+    return cases
+
+
+@pytest.mark.parametrize("case", _int_cases(), ids=lambda c: c["source"])
+def test_dec_int_reference_vectors(case):
+    """test/test_int.c:19-183 (tests[] and test_overlong_integer_full_buffer,
+    extracted by make_golden.py): the pre-parse's integer decoder
+    (qhuff_frames.cpp dec_int, exported as qhuff_dec_int) returns the
+    reference's value for every 0 vector, QHUFF_EPROTO for every -2, and
+    QHUFF_ETRUNC for every strict prefix (the reference's -1 loop,
+    test_int.c:202-208).  Then each vector is driven through the scanners
+    themselves: as a field section's Required Insert Count (8-bit prefix) or
+    S + Delta Base (7-bit), and as an encoder-stream Set Dynamic Table
+    Capacity (5-bit)."""
+    enc = bytes.fromhex(case["encoded"])
+    pb, ret = case["prefix_bits"], case["retval"]
+    assert ret in (0, -2)
+    rc, val, used = qhuff.dec_int(enc, pb)
+    if ret == 0:
+        assert (rc, val, used) == (qhuff.OK, int(case["decoded"]), len(enc))
+        # the Python restatement the fuzz tests use agrees
+        assert Q.dec_int(enc, 0, pb) == (int(case["decoded"]), len(enc))
+    else:
+        assert rc == qhuff.EPROTO
+        with pytest.raises(Q.ProtoError):
+            Q.dec_int(enc, 0, pb)
+    # strict prefixes: -1 from the reference; past 1 + 10 bytes the loop
+    # of lsqpack.c:2405-2425 stops reading (M = 70) and decides there
+    nfix = min(len(enc), 11) if case.get("whole") else len(enc)
+    for k in range(nfix):
+        assert qhuff.dec_int(enc[:k], pb)[0] == qhuff.ETRUNC, k
+    for k in range(nfix, len(enc)):
+        assert qhuff.dec_int(enc[:k], pb)[0] == rc, k
+    want = qhuff.OK if ret == 0 else qhuff.EPROTO
+    if pb in (7, 8):
+        # field section: RIC (8) then delta base (7); the vectors' bits above
+        # a 7-bit prefix are 0 (S = 0)
+        assert pb == 8 or enc[0] & 0x80 == 0
+        wrap = (lambda b: b + b"\x00") if pb == 8 else (lambda b: b"\x00" + b)
+        assert qhuff.scan_field_section(wrap(enc))[0] == want
+        assert Q.ref_scan_field_section(wrap(enc))[0] == \
+            ("ok" if ret == 0 else "proto")
+        # (a strict prefix of the RIC is the whole section: a delta-base byte
+        # after it would be read as its next continuation byte)
+        pre = (lambda b: b) if pb == 8 else wrap
+        for k in range(nfix):
+            assert qhuff.scan_field_section(pre(enc[:k]))[0] == qhuff.ETRUNC
+    if pb == 5:
+        # encoder stream: 001xxxxx Set Dynamic Table Capacity (lsqpack_dec_int,
+        # no 2^24 limit); a partial instruction is left unconsumed
+        assert enc[0] & 0xe0 == 0
+        ins = bytes([enc[0] | 0x20]) + enc[1:]
+        rc, lits, used = qhuff.scan_encoder_stream(ins)
+        assert (rc, lits, used) == ((qhuff.OK, [], len(ins)) if ret == 0
+                                    else (qhuff.EPROTO, [], 0))
+        for k in range(1, len(ins)):
+            assert qhuff.scan_encoder_stream(ins[:k]) == (qhuff.OK, [], 0)
+
+
+def test_dec_int_args():
+    assert qhuff.dec_int(b"\x01", 0)[0] == qhuff.EINVAL
+    assert qhuff.dec_int(b"\x01", 9)[0] == qhuff.EINVAL
+    # bits above the prefix are ignored
+    assert qhuff.dec_int(b"\xea", 5) == (qhuff.OK, 10, 1)
+
+
 def field_line(first, prefix_bits, payload, huffman=False):
     """one string literal: H bit above an N-bit prefixed length, then the
     payload (RFC 9204 4.5.4 / 4.5.6 shapes)"""
@@ -289,34 +366,70 @@ def test_gpu_decode_literals_with_errors(codec):
             assert st == 0 and o == payload
 
 
+def static_name_len(idx):
+    with open(os.path.join(G, "qpack_static_table.json")) as f:
+        return len(json.load(f)["static_table"][idx][0])
+
+
 @pytest.mark.gpu
 def test_gpu_decode_clamp(codec):
-    """header_out_grow_buf (lsqpack.c:3350-3351): a field-section string
-    never decodes past LSXPACK_MAX_STRLEN.  65,535 and 65,536 'a's (5-bit
-    code) both fit a 40,960-byte Huffman payload, declared well under the
-    limit: the scan accepts both, the literal decode with
-    max_len = MAX_STRLEN keeps the first and rejects the second, and
-    without a limit (encoder-stream use) decodes both.  The reference's
-    over-long declared lengths (test_header_alloc_clamp.c) never reach the
-    decode: the scan rejects their blocks."""
+    """header_out_grow_buf (lsqpack.c:3346-3351): a field line's name and
+    value are decoded into ONE header buffer that never grows past
+    LSXPACK_MAX_STRLEN (round 5 applied the limit to each
+    string alone).  With max_len = MAX_STRLEN: a literal name 'nm' takes 2
+    of the 65,535 bytes, so a value of 65,533 decoded bytes fits and 65,535
+    or 65,536 do not; a static name reference (lsqpack.c:3620-3642 copies
+    the table's name into the buffer) takes its name's length; a dynamic
+    reference (table with the reference) leaves the value checked alone.
+    Without a limit (encoder-stream use) everything decodes.  The
+    reference's over-long declared lengths (test_header_alloc_clamp.c)
+    never reach the decode: the scan rejects their blocks."""
     for case in clamp_kat()["cases"]:
         assert qhuff.scan_field_section(bytes.fromhex(case["block"]))[0] \
             == qhuff.EPROTO
-    buf, lits = b"", []
-    for n in (65535, 65536, 10, 0):
+    buf, lits, want = b"", [], []
+    # (huffman name?, name part, decoded value length, expected statuses)
+    nm_h = O.huffman_enc(b"nm")
+    cases = [(field_line(0x20, 3, b"nm"), 65533, [0, 0]),
+             (field_line(0x20, 3, b"nm"), 65534, [0, 1]),
+             (field_line(0x20, 3, b"nm"), 65535, [0, 1]),
+             (field_line(0x20, 3, b"nm"), 65536, [0, 1]),
+             (field_line(0x20, 3, nm_h, huffman=True), 65533, [0, 0]),
+             (field_line(0x20, 3, nm_h, huffman=True), 65534, [0, 1]),
+             (field_line(0x20, 3, b"nm"), 10, [0, 0]),
+             (field_line(0x20, 3, b"nm"), 0, [0, 0]),
+             # static name refs: index 0 (:authority, 10), 2 (age, 3), 31
+             # (a two-byte index)
+             (b"\x50", 65535 - static_name_len(0), [0]),
+             (b"\x50", 65536 - static_name_len(0), [1]),
+             (b"\x52", 65535 - static_name_len(2), [0]),
+             (b"\x52", 65536 - static_name_len(2), [1]),
+             (Q.enc_int(0x50, 31, 4), 65535 - static_name_len(31), [0]),
+             (Q.enc_int(0x50, 31, 4), 65536 - static_name_len(31), [1]),
+             # dynamic name ref (T = 0) and post-base name ref: value alone
+             (b"\x45", 65535, [0]),
+             (b"\x45", 65536, [1]),
+             (b"\x02", 65535, [0])]
+    for head, n, st in cases:
         h = O.huffman_enc(b"a" * n)
-        blk = (b"\x00\x00" + field_line(0x20, 3, b"nm")
-               + field_line(0, 7, h, huffman=True))
+        blk = b"\x00\x00" + head + field_line(0, 7, h, huffman=True)
         rc, ls = qhuff.scan_field_section(blk, len(buf))
-        assert rc == qhuff.OK
+        assert rc == qhuff.OK and len(ls) == len(st)
         buf += blk
         lits += ls
+        want += [(s_, n if (s_ == 0 and l.kind == qhuff.LIT_VALUE) else None)
+                 for s_, l in zip(st, ls)]
     outs, status = codec.decode_literals_host(buf, lits, qhuff.MAX_STRLEN)
-    assert list(status) == [0, 0, 0, 1, 0, 0, 0, 0]
-    assert outs[1] == b"a" * 65535 and outs[3] == b""
-    assert outs[5] == b"a" * 10 and outs[7] == b""
+    assert list(status) == [s_ for s_, _ in want]
+    for o, (s_, n), l in zip(outs, want, lits):
+        if s_:
+            assert o == b""
+        elif n is not None:
+            assert o == b"a" * n
+        else:
+            assert o == b"nm"
     outs, status = codec.decode_literals_host(buf, lits)
-    assert not status.any() and outs[3] == b"a" * 65536
+    assert not status.any()
     # a raw literal above the limit (only reachable through hand-made spans)
     raw = [qhuff.Literal(0, 70000, 0, 7, 2, 0, 0)]
     outs, status = codec.decode_literals_host(b"z" * 70000, raw,
