@@ -257,16 +257,19 @@ fail(qhuff_ctx *c, hipError_t e, const char *what)
 // of any context and freed with the last context that used it.  So a
 // context's own device memory stays small (tables, look-back flags, its
 // staging), however many contexts a process opens.  Contexts order their
-// launches on the pool: each launch on it records the pool's event, and a
-// launch of another context waits for it first (a context's own launches
-// are ordered by prepare_launch).  So a context that joins a pool in use
-// orders its first launch after the last one on it with a stream wait --
-// no device synchronisation, which would also wait for other libraries'
-// streams and a resident service kernel, under the pool's lock (ADVICE
-// r05) -- and a pool outgrown by a larger grid is retired, not freed,
-// until its last user closes.  Launches of different contexts on the pool
-// are serialised this way even when they write no slot (INTEGRATION.md
-// section 6).
+// launches on the pool: the pool remembers the context and stream of its
+// last launch, and a launch of another context first records the pool's
+// event on that stream and waits for it (a context's own launches are
+// ordered by prepare_launch).  Nothing is recorded while one context uses
+// the pool -- an event record after every launch cost the bench line 4 %
+// (683-689 against 713-720 GB/s, profiles/r06_c) -- and a context that
+// joins a pool in use needs no device synchronisation, which would also
+// wait for other libraries' streams and a resident service kernel, under
+// the pool's lock (only if recording on the last launch's
+// stream fails, e.g. the caller destroyed it, is the device synchronised).
+// A pool outgrown by a larger grid is retired, not freed, until its last
+// user closes.  Launches of different contexts on the pool are serialised
+// this way even when they write no slot.
 constexpr uint32_t kSmallGrid = 8;
 constexpr uint64_t kWaveSlotBytes = (uint64_t) kBigSlots * kBigSlotBytes;
 constexpr int kMaxDevices = 64;
@@ -277,19 +280,22 @@ struct SlotPool
     uint8_t *p = nullptr;
     uint64_t waves = 0;                  // slots for this many waves
     int refs = 0;                        // contexts that used it
-    hipEvent_t ev = nullptr;             // the last launch on it
-    const qhuff_ctx *ev_ctx = nullptr;   // whose launch ev follows
+    hipEvent_t ev = nullptr;             // (recorded at a context switch)
+    const qhuff_ctx *last_ctx = nullptr; // the last launch on it: its context
+    hipStream_t last_st = nullptr;       // and stream
     std::vector<uint8_t *> retired;      // outgrown pools (freed with it)
 };
 static SlotPool g_pool[kMaxDevices];
 
 static void
-pool_release(int device)
+pool_release(int device, const qhuff_ctx *c)
 {
     if (device < 0 || device >= kMaxDevices)
         return;
     SlotPool &sp = g_pool[device];
     std::lock_guard<std::mutex> g(sp.mu);
+    if (sp.last_ctx == c)                // (its launches have completed)
+        sp.last_ctx = nullptr;
     if (--sp.refs > 0)
         return;
     if (sp.p)
@@ -302,7 +308,6 @@ pool_release(int device)
     sp.p = nullptr;
     sp.waves = 0;
     sp.ev = nullptr;
-    sp.ev_ctx = nullptr;
 }
 
 static uint64_t
@@ -375,15 +380,26 @@ with_slots(qhuff_ctx *c, uint32_t grid, uint64_t wpb, bool *full,
         }
         sp.waves = w;
     }
-    if (sp.ev && sp.ev_ctx && sp.ev_ctx != c)
-        HIPCHK(c, hipStreamWaitEvent(st, sp.ev, 0));
+    if (sp.last_ctx && sp.last_ctx != c)
+    {
+        // after the pool's last launch, another context's: everything on
+        // its stream so far
+        if (!sp.ev)
+            HIPCHK(c, hipEventCreateWithFlags(&sp.ev, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(sp.ev, sp.last_st);
+        if (e == hipSuccess)
+            e = hipStreamWaitEvent(st, sp.ev, 0);
+        if (e != hipSuccess)
+        {
+            (void) hipGetLastError();
+            HIPCHK(c, hipDeviceSynchronize());
+        }
+    }
     const int rc = launch(sp.p);
     if (rc == QHUFF_OK)
     {
-        if (!sp.ev)
-            HIPCHK(c, hipEventCreateWithFlags(&sp.ev, hipEventDisableTiming));
-        HIPCHK(c, hipEventRecord(sp.ev, st));
-        sp.ev_ctx = c;
+        sp.last_ctx = c;
+        sp.last_st = st;
     }
     return rc;
 }
@@ -529,7 +545,7 @@ qhuff_close(qhuff_ctx *c)
     if (c->big_small)
         (void) hipFree(c->big_small);
     if (c->pool_ref)
-        pool_release(c->device);
+        pool_release(c->device, c);
     if (c->rare_host)
         (void) hipHostFree(c->rare_host);
     if (c->err)
