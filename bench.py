@@ -590,11 +590,12 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
     first decode launch, timed right after 8 token launches of each kind on
     the same context -- no launch on the batch itself before it (its
     Huffman form is made on a second context; the code objects are loaded
-    by the earlier legs).  By history (enc / dec: the device-pointer calls'
-    default, qhuff_host.cpp pick_full) that launch runs lean, ~2.6 ms /
-    ~0.7 ms on the corpus; hinted_*: the same with the variant hinted from
-    the host's copy of the offsets (qhuff_batch_hint, as the host-memory
-    calls do themselves)."""
+    by the earlier legs).  Unhinted (the device-pointer calls' default,
+    qhuff_host.cpp pick_full) that launch runs the full kernel (round 6;
+    until round 5 decode went by a history of earlier launches and ran
+    lean: 4.3x its warmed time on the corpus); hinted_*: the same with the
+    variant hinted from the host's copy of the offsets (qhuff_batch_hint,
+    as the host-memory calls do themselves)."""
     from qhuff import workload as W
     K = 10
     data_dir = os.path.join(ROOT, "tests", "golden", "data")
@@ -620,8 +621,7 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
            "synthetic_token_gbps": round(syn_gbps, 1)}
     # each batch's Huffman form (the decode legs' input) made on a context
     # of its own: on `codec` that launch would be a launch on the batch
-    # before its first-launch measurement (its rare-tile report sets the
-    # variant history)
+    # before its first-launch measurement
     prep = qhuff.Codec(dev.index or 0)
     for name, desc, (data, off) in batches:
         raw = int(off[-1])
@@ -640,8 +640,8 @@ def run_workloads(args, np, torch, qhuff, codec, dev, stream, n, raw_syn,
         doo = torch.empty(n + 1, dtype=torch.int32, device=dev)
         st = torch.empty(n, dtype=torch.uint8, device=dev)
         # the first launch of each kind on this batch, after 8 token
-        # launches of each kind, each waited for (the history counts
-        # launches seen to have run; the output is checked with the others')
+        # launches of each kind, each waited for (the output is checked
+        # with the others')
         for _ in range(8):
             codec.encode_into(s_in, s_off, n, 0, s_eo, s_eoo, stream)
             torch.cuda.synchronize()

@@ -55,8 +55,10 @@ extern "C" {
  *      qhuff_batch_needs_full (the kernel variant from the batch)
  *   7  qhuff_dec_int (the pre-parse's integer decoder); qhuff_decode_
  *      literals_ex applies max_len to a field line's name + value;
- *      qhuff_encode_batch_host_multi / qhuff_decode_batch_host_multi (one
- *      batch over several contexts / GPUs) */
+ *      qhuff_encode_batch_host_multi / qhuff_decode_batch_host_multi and
+ *      qhuff_*_batch_multi (one batch over several contexts / GPUs); an
+ *      unhinted launch runs the full kernel (decode's launch history is
+ *      gone) */
 #define QHUFF_ABI_VERSION 7
 
 /* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
@@ -417,19 +419,18 @@ int qhuff_timing_read(qhuff_ctx *ctx, uint32_t *kind, double *us, uint32_t max);
 
 /* Kernel variants.  Encode and decode each have a lean kernel and a full
  * one that also carries the big-tile slots and the cooperative long-string
- * decode.  By default (QHUFF_KERNELS=auto) the variant comes from the batch
- * when the library or the caller knows it (the host-memory calls; a hint,
- * below); otherwise encode launches its full kernel, and decode the lean
- * one until a launch reports such tiles, then the full one until 8
- * launches have been seen to run without any (QHUFF_KERNELS=lean|full pins
- * one).  Returns 1 if the context's last launch of `kind`
+ * decode.  By default (QHUFF_KERNELS=auto) a launch runs the full kernel,
+ * unless its batch is known to need only the lean one: the host-memory calls
+ * read their offsets, a device-pointer caller may pass a hint (below);
+ * QHUFF_KERNELS=lean|full pins one.  (Until ABI 6 decode chose by a history
+ * of earlier launches.)  Returns 1 if the context's last launch of `kind`
  * (QHUFF_KIND_ENCODE / QHUFF_KIND_DECODE) ran the full kernel, 0 if the
  * lean one or none yet, QHUFF_EINVAL otherwise.  Diagnostic: the output
  * bytes are the same either way. */
 int qhuff_kernel_variant(qhuff_ctx *ctx, int kind);
 
 /* (ABI 6) The variant of the next launch of `kind` from what the caller
- * knows of its batch, instead of the history above: hint 1 = the batch has
+ * knows of its batch: hint 1 = the batch has
  * a string longer than 128 bytes or a 64-string tile spanning more than the
  * kernels' 3 KB stage (the full kernel), 0 = it has none (the lean one),
  * -1 = no hint.  Applies to the next launch of that kind only.  The host-

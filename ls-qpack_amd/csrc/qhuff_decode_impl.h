@@ -1050,8 +1050,6 @@ struct DecPolicyT
     QH_LDS DecWave *wv;
     uint32_t slot0;                  // this lane's arena slot (current tile)
     uint64_t coop = 0;               // strings decoded by the whole wave
-    bool hint = false;               // the tile has a string for coop_phase
-    __device__ __forceinline__ bool rare_hint() const { return hint; }
 #ifdef QHUFF_PROFILE
     const Coord *pc = nullptr;       // (profiling) stamps of coop_decode
 #endif
@@ -1093,7 +1091,6 @@ struct DecPolicyT
         // the slots end below kVarArenaBytes - slack + 1 for this span; the
         // bitmap (hl / 4 + 2 words) and the sinks go above them
         // (at most 48 cooperative strings: at least 16 lanes for segments)
-        hint = !fixed && __builtin_amdgcn_ballot_w64(valid & (hl > kCoopMin));
         const bool cand = kCoop && !fixed && valid && hl > kCoopMin;
         coop = __builtin_amdgcn_ballot_w64(cand);
         if (__builtin_popcountll(coop) > 48)
@@ -1199,6 +1196,12 @@ struct DecPolicyT
                                               uint32_t &sz, uint32_t &st,
                                               uint8_t *dst)
     {
+#if QH_COOP_VIA_BIG
+        // a staged tile whose codec left strings for the whole wave
+        // (qhuff_pipeline.h): their cooperative phase here
+        if (kCoop && sp.staged && coop)
+            coop_phase(to, 0, cnt, sp, &sz, &st);
+#endif
         return dec_big_sizes<Keep>(in, sm, wv, cnt, to, sp, sz, st, slot0, dst);
     }
     // a big tile whose output does not fit a slot (qhuff_pipeline.h), after

@@ -97,12 +97,6 @@ struct Coord
                                             // the grid covers; qhuff_pipeline.h)
     uint8_t *big;                           // big-tile output slots:
                                             // kBigSlots per wave of the grid
-    uint32_t *rare;                         // host-mapped words: [0] set
-                                            // when the launch met tiles the
-                                            // full kernel is for, [1] the
-                                            // epoch of the launch once it
-                                            // started (qhuff_host.cpp
-                                            // pick_full)
 };
 
 // A big tile's output (qhuff_pipeline.h) waits in one of its wave's
@@ -117,10 +111,24 @@ static_assert(kWaves <= (int) kBigMaxWaves, "big-tile slots per workgroup");
 struct Coord;
 __device__ __forceinline__ void raise_error(const Coord &c, uint32_t bits);
 
+// The lane id is opaque to the optimiser (round 6): a per-lane address
+// computed from it (a big-tile slot, a 16-byte chunk of a copy) is then
+// rebuilt where it is used, not computed once before the tile loop and
+// kept -- spilled -- across it.  Full encode 18 -> 2 spilled VGPRs, full
+// decode 11 -> 2 (profiles/r06_f).
+#ifndef QH_OPAQUE_LANE
+#define QH_OPAQUE_LANE 1
+#endif
 __device__ __forceinline__ uint32_t
 lane_id()
 {
+#if QH_OPAQUE_LANE
+    uint32_t v = threadIdx.x & 63;
+    asm volatile("" : "+v"(v));
+    return v;
+#else
     return threadIdx.x & 63;
+#endif
 }
 
 __device__ __forceinline__ uint32_t
@@ -401,7 +409,7 @@ struct Span
 {
     uintptr_t pa;
     uint32_t n16;
-    bool staged;
+    uint32_t staged;                 // (wave-uniform; see Pending::valid)
 };
 
 __device__ __forceinline__ Span

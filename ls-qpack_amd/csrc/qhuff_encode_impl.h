@@ -886,7 +886,6 @@ struct EncPolicyT
     static constexpr bool kBig = Full;
     static constexpr bool kCoop = false;          // (no coop_phase)
     static constexpr uint64_t coop = 0;
-    __device__ __forceinline__ bool rare_hint() const { return false; }
     static constexpr int kInCap = kEncInCap;
     static constexpr int kDepth = QH_ENC_DEPTH;       // pending tiles
     static constexpr int kOutCap = kEncOutCap;
@@ -900,7 +899,7 @@ struct EncPolicyT
     uint32_t rs, re;                 // this lane's string in the stage
     uint32_t ds, bits;               // its range of the dense stream
     EncSize z;
-    bool dense;                      // wave-uniform: tile from the dense stream
+    uint32_t dense;                  // wave-uniform: tile from the dense stream
 
     // staged tile: chunks into the LDS stage
     __device__ __forceinline__ void stage_in(const Chunks<kChunks> &ch,

@@ -164,21 +164,12 @@ struct qhuff_ctx
                                          // larger launches use the device's
                                          // pool (slot_pool)
     bool pool_ref;                       // holds a reference on that pool
-    // kernel variant per kind (0 encode, 1 decode; pick_full): from the
-    // batch when known (hint), else encode full and decode by history -- the
-    // lean kernel until a launch reports big tiles or long strings, then the
-    // full one (big-tile slots, cooperative long strings) until kCalm
-    // launches in a row have none
-    uint32_t *rare_host;                 // pinned, device-mapped: [2 kind],
-                                         // [2 kind + 1] (pick_full)
-    uint32_t *rare_dev;
-    bool full[2];
-    uint32_t calm[2];
-    uint32_t seen[2];                    // rare_host[2 kind + 1] last read
+    // kernel variant per kind (0 encode, 1 decode; pick_full): the full
+    // kernel unless the batch is known (a hint) to need only the lean one
     bool last_full[2];                   // variant of the last launch
     int hint[2];                         // the next launch's variant from
                                          // its batch, known on the host
-                                         // (host_hint), or -1: history
+                                         // (host_hint), or -1: full
     int kernels;                         // QHUFF_KERNELS: 0 auto, 1 lean,
                                          // 2 full
     unsigned long long *prof;            // QHUFF_PROFILE builds: stamp buffer
@@ -470,12 +461,7 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     if (e == hipSuccess)
         e = hipMemset(c->err, 0, kErrWords * sizeof(uint32_t));
     if (e == hipSuccess)
-        e = hipHostMalloc((void **) &c->rare_host, 4 * sizeof(uint32_t),
-                          hipHostMallocMapped | hipHostMallocCoherent);
-    if (e == hipSuccess)
     {
-        memset(c->rare_host, 0, 4 * sizeof(uint32_t));
-        e = hipHostGetDevicePointer((void **) &c->rare_dev, c->rare_host, 0);
         const char *kv = getenv("QHUFF_KERNELS");
         c->kernels = !kv ? 0 : !strcmp(kv, "lean") ? 1 : !strcmp(kv, "full") ? 2 : 0;
     }
@@ -546,8 +532,6 @@ qhuff_close(qhuff_ctx *c)
         (void) hipFree(c->big_small);
     if (c->pool_ref)
         pool_release(c->device, c);
-    if (c->rare_host)
-        (void) hipHostFree(c->rare_host);
     if (c->err)
         (void) hipFree(c->err);
     if (c->d_stage)
@@ -735,7 +719,6 @@ coord(qhuff_ctx *c, uint64_t tiles)
     k.n_tiles = (uint32_t) tiles;
     k.spread = 0;
     k.big = nullptr;                     // (with_slots)
-    k.rare = nullptr;
     return k;
 }
 
@@ -852,33 +835,24 @@ grid_for(const qhuff_ctx *c, uint64_t tiles, uint64_t waves_per_block,
     return (uint32_t) (need < cap ? need : cap);
 }
 
-// The kernel variant of the next launch of `kind` (0 encode, 1 decode),
-// and where it reports.  Per kind two words of pinned, device-mapped host
-// memory: [0] set by a launch that met big tiles or long strings (at its
-// end), [1] the epoch of the last launch that started (block 0, at its
-// start: every earlier launch of the stream has ended).  Both are read here
-// without waiting for any launch, so the switch to the full kernel lands a
-// launch or two after the data changes, and the way back needs kCalm
-// launches seen to have run -- not issued: a burst of launches is issued
-// long before the first of them reports.  (The lean kernel codes those
-// tiles correctly but slowly; the full one carries their code beside the
-// tile loop, which costs the loop 1.3 % (encode) / 3.3 % (decode) on
-// batches that never need it.
-// Choosing inside the launch instead -- each wave lean until its first
-// such tile, then full -- was built three ways in round 5 and measured
-// slower: DESIGN.md section 6.)
-static constexpr uint32_t kCalm = 8;
-// (round 5) without a hint, encode runs its full kernel: on the token batch
-// it costs +1.3 % against the lean one (the full kernels' rare branches
-// marked cold, qhuff_pipeline.h QH_RARE), while the lean one's first launch
-// on a long-string batch took 30x its warmed time (the QIF corpus, 2.1 ms:
-// big tiles out of line, one lane per string in global memory); decode
-// keeps the history (full +3.3 %, lean first launch 4.1x)
-static constexpr bool kHistory[2] = {false, true};
+// The kernel variant of the next launch of `kind` (0 encode, 1 decode).
+// The full kernel codes every batch at its best; the lean one (no big-tile
+// slots, no cooperative long-string decode: those tiles out of line, one
+// lane per string, up to 30x slower on the QIF corpus) is 0.7 % (encode) /
+// 1.3 % (decode) faster on batches that never need them (profiles/r06_i,
+// same-box pairs).  So: the full kernel, unless the caller's batch is known
+// to have no string over 128 bytes and no tile over the 3 KB stage -- the
+// host-memory calls read their offsets (host_hint), a device-pointer caller
+// may say so with qhuff_batch_hint -- or QHUFF_KERNELS pins one.  (Until
+// round 5 decode went by a history of earlier launches, lean until one
+// reported such tiles: the first launch of a long-string batch after token
+// batches then took 4.3x its warmed time.  Round 6 took the full decode
+// kernel's cost on the token batch from +3.3 % to +1.3 %: the lane id
+// opaque to the optimiser, uniform flags as u32, the cooperative phase on
+// the big-tile path)
 static bool
-pick_full(qhuff_ctx *c, int kind, Coord *k)
+pick_full(qhuff_ctx *c, int kind)
 {
-    k->rare = c->rare_dev + 2 * kind;
     // a hint applies to the next launch of its kind only, whatever decides
     // this one
     const int hint = c->hint[kind];
@@ -886,29 +860,8 @@ pick_full(qhuff_ctx *c, int kind, Coord *k)
     if (c->kernels)
         return c->last_full[kind] = c->kernels == 2;
     if (hint >= 0)
-        // the host path read this batch's offsets (host_hint): no history
         return c->last_full[kind] = hint > 0;
-    if (!kHistory[kind])
-        return c->last_full[kind] = true;
-    volatile uint32_t *r = c->rare_host + 2 * kind;
-    if (r[0])
-    {
-        r[0] = 0;
-        c->full[kind] = true;
-        c->calm[kind] = 0;
-        c->seen[kind] = r[1];
-    }
-    else if (c->full[kind])
-    {
-        const uint32_t s = r[1];
-        if (s != c->seen[kind])
-        {
-            c->seen[kind] = s;
-            if (++c->calm[kind] >= kCalm)
-                c->full[kind] = false;
-        }
-    }
-    return c->last_full[kind] = c->full[kind];
+    return c->last_full[kind] = true;
 }
 
 extern "C" int
@@ -950,7 +903,7 @@ qhuff_encode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     a.c = coord(c, tiles);
     const uint64_t wpb = (uint64_t) encode_waves_per_block();
     const uint32_t grid = grid_for(c, tiles, wpb, c->enc_grid, &a.c.spread);
-    bool full = pick_full(c, 0, &a.c);
+    bool full = pick_full(c, 0);
     rc = with_slots(c, grid, wpb, &full, st, [&](uint8_t *slots) -> int {
         a.c.big = slots;
         hipEvent_t e0, e1;
@@ -1002,7 +955,7 @@ qhuff_decode_batch(qhuff_ctx *c, const uint8_t *in, const uint32_t *in_off,
     // outside the variant choice of the batch kernel: ADVICE r04)
     bool full = false;
     if (!c->keep_rejected)
-        full = pick_full(c, 1, &a.c);
+        full = pick_full(c, 1);
     else
         c->hint[1] = -1;                 // (consumed by this launch too)
     rc = with_slots(c, grid, wpb, &full, st, [&](uint8_t *slots) -> int {

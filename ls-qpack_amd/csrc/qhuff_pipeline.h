@@ -57,6 +57,9 @@ namespace qhuff {
 // profiles/r05_cold); the lean kernels' loop is left as it was (the same
 // hints cost their decode ~1 %)
 #define QH_RARE(full, c) ((full) ? __builtin_expect((c), 0) : (c))
+#ifndef QH_COOP_VIA_BIG
+#define QH_COOP_VIA_BIG 1
+#endif
 
 constexpr int kChunks = 3;                  // 16-byte input chunks per lane
 constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: chunk registers / stages
@@ -67,7 +70,7 @@ constexpr int kStageCap = 64 * kChunks * 16;  // 3072 B: chunk registers / stage
 // per pending tile it cost ~14 VGPRs a tile.)
 struct Pending
 {
-    bool valid;
+    uint32_t valid;                  // (wave-uniform; a bool here is a lane mask)
     uint32_t excl;                   // this lane's tile-local output offset
     uint32_t stat;                   // this lane's status byte
     uint32_t tile, total;            // (wave-uniform)
@@ -421,11 +424,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
 {
     const QH_GLB uint32_t *in_off = (const QH_GLB uint32_t *) in_off_p;
     const uint32_t nt = c.n_tiles;
-    // the launch has started (qhuff_host.cpp pick_full: every earlier launch
-    // of the stream has ended, and reported)
-    if (c.rare && blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(c.rare + 1, c.epoch, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
     // this wave's first tile t0 and the tickets k1 < k2 of its next ones
     // (claimed for the whole block in the kernel prologue, or kClaimNow)
     uint32_t t = t0;
@@ -497,7 +495,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         pend[i].big = 0;
     }
     uint32_t big_next = 0;                   // big-tile slots used (ring)
-    bool rare = false;                       // met a big or cooperative tile
     uint32_t it = 0;
     for (;; ++it)
     {
@@ -569,12 +566,20 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
         {
             pol.prepare(sp_cur);
             pol.codec(o_cur, cnt, sp_cur, &sz, &st);
+#if QH_COOP_VIA_BIG
+            // a tile with strings for the whole wave goes the big tiles'
+            // way (P::big_sizes runs its cooperative phase): one copy of
+            // that code, beside the big-tile path, and the loop keeps the
+            // lean kernel's registers
+            if (QH_RARE(P::kBig, P::kCoop && pol.coop))
+                fast = false;
+#else
             if (QH_RARE(P::kBig, P::kCoop && pol.coop))
             {
                 park();
                 pol.coop_phase(o_cur, 0, cnt, sp_cur, &sz, &st);
             }
-            rare |= pol.rare_hint();
+#endif
         }
         uint32_t incl = wave_incl_scan(sz);
         uint32_t excl = incl - sz;
@@ -590,7 +595,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
             // resolves -- and the wave goes straight on to its next tile.
             if (QH_RARE(P::kBig, !fast))
             {
-                rare = true;
                 // the pending tiles' outputs move to slots first, so that their
                 // registers are free for the big tile's codec (the slots hold
                 // every tile in flight: kDepth pending + this one)
@@ -672,7 +676,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
             outs[D - 1].clear();             // (its output is in its slot)
         else
         {
-            rare = true;
             // (rare: a big tile in the lean kernel, or one whose output
             // exceeds a slot) coded out of line after the pending tiles are
             // flushed, so that no tile output is live across the call -- but
@@ -737,11 +740,6 @@ tile_pipeline(P &pol, const Coord &c, const Tickets &tk, uint32_t t0,
     // (The wave claimed until a claim landed past the end, so every ticket
     // of its group is taken, by running waves: see BlockTickets.  A spread
     // launch hands out a prefix of the tiles, one per wave.)
-    // the launch met tiles the full kernel is for: tell the host (one store
-    // per wave that did; qhuff_host.cpp picks the next launch's kernel)
-    if (rare && c.rare && lane_id() == 0)
-        __hip_atomic_store(c.rare, 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace qhuff

@@ -499,7 +499,7 @@ class Codec:
 
     def batch_hint(self, kind, hint):
         """qhuff_batch_hint: the next launch of kind runs the full (1) or
-        lean (0) kernel, or by history (-1)."""
+        lean (0) kernel, or no hint (-1: the full kernel)."""
         self._check(lib().qhuff_batch_hint(self._ctx, kind, hint),
                     "qhuff_batch_hint")
 
