@@ -215,7 +215,10 @@ stage_chunks(const Span &sp, QH_LDS u32x4 *dst)
 __device__ __forceinline__ uint8_t *
 big_slot(const Coord &c, uint32_t k)
 {
-    const uint64_t gid = (uint64_t) blockIdx.x * kWaves + (threadIdx.x >> 6);
+    // (wave-uniform, scalar: in a VGPR pair this address was computed
+    // before the tile loop and spilled across it)
+    const uint64_t gid = (uint64_t) blockIdx.x * kWaves
+                       + (uint32_t) __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     return c.big + (gid * kBigSlots + k) * (uint64_t) kBigSlotBytes;
 }
 
