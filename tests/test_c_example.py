@@ -84,3 +84,27 @@ def test_hook_decoder_seam_matches_lsqpack_huff_decode():
                        text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+
+
+# ---- examples/multi_demo.c: one batch over several contexts from plain C ---
+
+MULTI = os.path.join(EX, "multi_demo")
+
+
+def test_multi_demo_builds_and_links():
+    subprocess.check_call(["make", "-s", "-C", EX])
+    out = subprocess.check_output(["ldd", MULTI]).decode()
+    assert "libqhuff.so" in out and "not found" not in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("g", [1, 2, 3])
+def test_multi_demo_round_trip(g):
+    """qhuff_encode_batch_host_multi / qhuff_decode_batch_host_multi from a
+    plain C99 caller: G contexts (round-robin over the visible devices),
+    the stitched encode equals a one-context encode byte for byte and the
+    stitched decode equals the input"""
+    r = subprocess.run([MULTI, str(g), "100003"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
