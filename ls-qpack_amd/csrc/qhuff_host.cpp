@@ -1453,16 +1453,30 @@ ctxs_ok(qhuff_ctx *const *ctxs, uint32_t g)
 
 // run f(k) for k in [0, g): threads for k >= 1, the caller for k = 0;
 // the first failing return code (in shard order), or QHUFF_OK
+// (A shard whose thread cannot be created runs on the caller's thread after
+// shard 0, in shard order: a shard only ever waits for earlier ones.)
 template <class F>
 static int
 run_shards(uint32_t g, F f)
 {
     std::vector<int> rc(g, QHUFF_OK);
     std::vector<std::thread> th;
+    std::vector<uint32_t> inline_k;
     th.reserve(g ? g - 1 : 0);
     for (uint32_t k = 1; k < g; ++k)
-        th.emplace_back([&rc, &f, k] { rc[k] = f(k); });
+    {
+        try
+        {
+            th.emplace_back([&rc, &f, k] { rc[k] = f(k); });
+        }
+        catch (...)
+        {
+            inline_k.push_back(k);
+        }
+    }
     rc[0] = f(0);
+    for (uint32_t k : inline_k)
+        rc[k] = f(k);
     for (auto &t : th)
         t.join();
     for (uint32_t k = 0; k < g; ++k)
