@@ -457,6 +457,33 @@ def main():
                         "staging copies (copy workers) + hipMemcpyAsync in + "
                         "kernel + exact-size hipMemcpyAsync out, synchronous, "
                         "best of 5 after one sizing call"}
+        # the same calls with every buffer registered (qhuff_host_register):
+        # DMA straight from / into the caller's memory, no staging copy
+        for a in (eo, eoo, do, doo, dst):
+            a.fill(1)
+        t = time.perf_counter()
+        with qhuff.registered(data, off, h_np, h_off_np, eo, eoo, do, doo,
+                              dst):
+            t_reg = time.perf_counter() - t
+            t_e = t_d = 1e30
+            for _ in range(5):
+                t = time.perf_counter()
+                codec.encode_host(data, off, 0, eo, eoo)
+                t_e = min(t_e, time.perf_counter() - t)
+                t = time.perf_counter()
+                codec.decode_host(h_np, h_off_np, do, doo, dst)
+                t_d = min(t_d, time.perf_counter() - t)
+        ok_reg = (np.array_equal(doo, off) and not dst.any()
+                  and np.array_equal(do[:raw_bytes], data)
+                  and np.array_equal(eoo, h_off_np)
+                  and np.array_equal(eo[:int(eoo[-1])], h_np))
+        host["registered"] = {
+            "enc_gbps": round(raw_bytes / t_e / 1e9, 3),
+            "dec_gbps": round(raw_bytes / t_d / 1e9, 3),
+            "enc_ms": round(t_e * 1e3, 3), "dec_ms": round(t_d * 1e3, 3),
+            "register_ms": round(t_reg * 1e3, 3), "roundtrip_ok": bool(ok_reg),
+            "note": "all nine buffers registered once (register_ms, not in "
+                    "the calls): hipMemcpyAsync from / into them directly"}
 
     # ---- CPU baseline (rank 0, N = 1 only), after every GPU leg: seconds of
     # an idle GPU before a leg slow its first launches (the hash leg's mean

@@ -58,7 +58,8 @@ extern "C" {
  *      qhuff_encode_batch_host_multi / qhuff_decode_batch_host_multi and
  *      qhuff_*_batch_multi (one batch over several contexts / GPUs); an
  *      unhinted launch runs the full kernel (decode's launch history is
- *      gone) */
+ *      gone); qhuff_host_register / qhuff_host_unregister (direct DMA for
+ *      the host-memory calls) */
 #define QHUFF_ABI_VERSION 7
 
 /* QHUFF_ABI_VERSION of the loaded library (compare with the header's) */
@@ -138,6 +139,20 @@ int qhuff_encode_batch_host(qhuff_ctx *ctx, const uint8_t *in,
 int qhuff_decode_batch_host(qhuff_ctx *ctx, const uint8_t *in,
                             const uint32_t *in_off, uint32_t n, uint8_t *out,
                             uint32_t *out_off, uint8_t *status);
+
+/* (ABI 7) Register caller buffers for direct DMA by the host-memory calls
+ * (hipHostRegister, portable to every device; process-wide).  When a host
+ * call's input bytes and offsets lie in registered ranges they are
+ * transferred to the device directly, without the pinned staging copy; when
+ * its output buffer (the bound), offsets and statuses do, the results are
+ * transferred straight into them.  Register long-lived buffers once (it pins
+ * their pages: milliseconds for tens of MB); the results are the same either
+ * way.  qhuff_host_register: QHUFF_OK, QHUFF_EINVAL (null, 0 bytes, or ptr
+ * already registered), QHUFF_ENOMEM / QHUFF_EDEVICE (the reason in
+ * qhuff_last_error(NULL)).  qhuff_host_unregister: ptr as registered; no call
+ * may be using it. */
+int qhuff_host_register(void *ptr, size_t bytes);
+int qhuff_host_unregister(void *ptr);
 
 /* ---- low-latency service ----------------------------------------------
  * The reference codes one literal per call, a few dozen per header block

@@ -1206,6 +1206,74 @@ struct ShardSync
     }
 };
 
+// ---- caller buffers registered for direct DMA (qhuff_host_register) -------
+//
+// The host path stages the caller's input into pinned memory and its output
+// back out of it: ~67 MB of host memcpy for a 1M-string encode + decode,
+// which bounds it near the copy workers' rate (~22 GB/s of payload each way,
+// DESIGN.md section 5).  Buffers the caller registered once (hipHostRegister,
+// portable: every device's DMA engines reach them) are read and written by
+// the transfers directly: no staging copy, and the path is bound by PCIe.
+struct HostReg
+{
+    std::mutex mu;
+    std::vector<std::pair<uintptr_t, uintptr_t>> r;      // [begin, end)
+};
+static HostReg g_reg;
+
+static bool
+host_registered(const void *p, uint64_t bytes)
+{
+    if (!bytes)
+        return true;
+    const uintptr_t a = (uintptr_t) p, b = a + bytes;
+    std::lock_guard<std::mutex> g(g_reg.mu);
+    for (const auto &x : g_reg.r)
+        if (x.first <= a && b <= x.second)
+            return true;
+    return false;
+}
+
+extern "C" int
+qhuff_host_register(void *ptr, size_t bytes)
+{
+    if (!ptr || !bytes)
+        return QHUFF_EINVAL;
+    std::lock_guard<std::mutex> g(g_reg.mu);
+    for (const auto &x : g_reg.r)
+        if (x.first == (uintptr_t) ptr)
+            return QHUFF_EINVAL;         // (already registered)
+    const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterPortable);
+    if (e != hipSuccess)
+    {
+        (void) hipGetLastError();
+        snprintf(t_open_err, sizeof(t_open_err), "hipHostRegister: %s",
+                 hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? QHUFF_ENOMEM : QHUFF_EDEVICE;
+    }
+    g_reg.r.emplace_back((uintptr_t) ptr, (uintptr_t) ptr + bytes);
+    return QHUFF_OK;
+}
+
+extern "C" int
+qhuff_host_unregister(void *ptr)
+{
+    std::lock_guard<std::mutex> g(g_reg.mu);
+    for (size_t i = 0; i < g_reg.r.size(); ++i)
+        if (g_reg.r[i].first == (uintptr_t) ptr)
+        {
+            const hipError_t e = hipHostUnregister(ptr);
+            g_reg.r.erase(g_reg.r.begin() + (ptrdiff_t) i);
+            if (e != hipSuccess)
+            {
+                (void) hipGetLastError();
+                return QHUFF_EDEVICE;
+            }
+            return QHUFF_OK;
+        }
+    return QHUFF_EINVAL;
+}
+
 static int
 host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
            uint32_t n, unsigned mode, uint8_t *out, uint32_t *out_off,
@@ -1258,18 +1326,36 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
     hipStream_t sk = c->own_stream;
     uint64_t base = 0;                           // output bytes so far
     uint32_t tot[kMaxChunks];
+    uint64_t obase[kMaxChunks];                  // chunk i's output start
+    uint64_t fbase = 0;                          // (relative to the call's)
     // a small batch brings its whole output bound back right behind the
     // kernel: one synchronisation instead of two (latency, not bandwidth)
     const bool small = K == 1 && ob[1] <= (4u << 20);
+    // caller buffers registered for DMA (qhuff_host_register): transferred
+    // directly, no staging copy
+    const bool din = host_registered(in + a0, in_bytes)
+                  && host_registered(in_off, 4ull * (n + 1));
+    const bool dout = !small
+        && host_registered(out, enc ? qhuff_encode_bound(in_bytes, n, mode)
+                                    : qhuff_decode_bound(in_bytes, n))
+        && host_registered(out_off, 4ull * (n + 1))
+        && (enc || host_registered(status, n));
 
     auto stage_in = [&](unsigned i) -> int {
         const uint32_t s0 = cut[i], s1 = cut[i + 1];
         const uint64_t b0 = in_off[s0] - a0, b1 = in_off[s1] - a0;
-        c->pool->copy(H + o_in + b0, in + a0 + b0, b1 - b0);
-        memcpy(H + o_off + 4ull * s0, in_off + s0, 4ull * (s1 - s0 + 1));
-        HIPCHK(c, hipMemcpyAsync(D + o_in + b0, H + o_in + b0, b1 - b0,
+        const uint8_t *src_in = in + a0;
+        const uint8_t *src_off = (const uint8_t *) in_off;
+        if (!din)
+        {
+            c->pool->copy(H + o_in + b0, in + a0 + b0, b1 - b0);
+            memcpy(H + o_off + 4ull * s0, in_off + s0, 4ull * (s1 - s0 + 1));
+            src_in = H + o_in;
+            src_off = H + o_off;
+        }
+        HIPCHK(c, hipMemcpyAsync(D + o_in + b0, src_in + b0, b1 - b0,
                                  hipMemcpyHostToDevice, c->h2d_stream));
-        HIPCHK(c, hipMemcpyAsync(D + o_off + 4ull * s0, H + o_off + 4ull * s0,
+        HIPCHK(c, hipMemcpyAsync(D + o_off + 4ull * s0, src_off + 4ull * s0,
                                  4ull * (s1 - s0 + 1), hipMemcpyHostToDevice,
                                  c->h2d_stream));
         HIPCHK(c, hipEventRecord(c->ev_in[i], c->h2d_stream));
@@ -1285,35 +1371,76 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
                                          sk);
         if (r)
             return r;
-        HIPCHK(c, hipMemcpyAsync(H + o_oo + 4ull * (s0 + i), doo,
-                                 4ull * (s1 - s0 + 1), hipMemcpyDeviceToHost, sk));
-        if (!enc)
-            HIPCHK(c, hipMemcpyAsync(H + o_st + s0, D + o_st + s0, s1 - s0,
+        if (dout)
+        {
+            // the chunk-local offsets straight into out_off (rebased in
+            // place by unstage), the chunk's total into the stage
+            HIPCHK(c, hipMemcpyAsync(out_off + s0, doo, 4ull * (s1 - s0),
                                      hipMemcpyDeviceToHost, sk));
+            HIPCHK(c, hipMemcpyAsync(H + o_oo + 4ull * (s1 + i), doo + (s1 - s0),
+                                     4, hipMemcpyDeviceToHost, sk));
+            if (!enc)
+                HIPCHK(c, hipMemcpyAsync(status + s0, D + o_st + s0, s1 - s0,
+                                         hipMemcpyDeviceToHost, sk));
+        }
+        else
+        {
+            HIPCHK(c, hipMemcpyAsync(H + o_oo + 4ull * (s0 + i), doo,
+                                     4ull * (s1 - s0 + 1), hipMemcpyDeviceToHost,
+                                     sk));
+            if (!enc)
+                HIPCHK(c, hipMemcpyAsync(H + o_st + s0, D + o_st + s0, s1 - s0,
+                                         hipMemcpyDeviceToHost, sk));
+        }
         if (small)
             HIPCHK(c, hipMemcpyAsync(H + o_out, D + o_out, ob[1],
                                      hipMemcpyDeviceToHost, sk));
         HIPCHK(c, hipEventRecord(c->ev_k[i], sk));
         return QHUFF_OK;
     };
+    // chunk i's output bytes back: to the stage, or (dout) straight to
+    // out + dst (once its base is known)
+    auto issue_out = [&](unsigned i, uint64_t dst) -> int {
+        HIPCHK(c, hipStreamWaitEvent(c->d2h_stream, c->ev_k[i], 0));
+        if (tot[i])
+            HIPCHK(c, hipMemcpyAsync(dout ? out + dst : H + o_out + ob[i],
+                                     D + o_out + ob[i], tot[i],
+                                     hipMemcpyDeviceToHost, c->d2h_stream));
+        HIPCHK(c, hipEventRecord(c->ev_out[i], c->d2h_stream));
+        return QHUFF_OK;
+    };
     auto fetch = [&](unsigned i) -> int {
         HIPCHK(c, hipEventSynchronize(c->ev_k[i]));
         const uint32_t s1 = cut[i + 1];
         tot[i] = ((const uint32_t *) (H + o_oo))[s1 + i];
+        obase[i] = fbase;
+        fbase += tot[i];
         if (small)
             return QHUFF_OK;                     // already here
-        HIPCHK(c, hipStreamWaitEvent(c->d2h_stream, c->ev_k[i], 0));
-        if (tot[i])
-            HIPCHK(c, hipMemcpyAsync(H + o_out + ob[i], D + o_out + ob[i],
-                                     tot[i], hipMemcpyDeviceToHost,
-                                     c->d2h_stream));
-        HIPCHK(c, hipEventRecord(c->ev_out[i], c->d2h_stream));
-        return QHUFF_OK;
+        // (a shard of a multi-context call learns its base only later: its
+        // direct copies out wait for it)
+        if (dout && sync)
+            return QHUFF_OK;
+        return issue_out(i, obase[i]);
     };
     auto unstage = [&](unsigned i) -> int {
         if (!small)
             HIPCHK(c, hipEventSynchronize(c->ev_out[i]));
         const uint32_t s0 = cut[i], s1 = cut[i + 1];
+        if (dout)
+        {
+            // bytes and statuses are in place; the offsets get the base
+            const uint32_t bs = (uint32_t) base;
+            const uint32_t m = s1 - s0, sl = 1u << 16;
+            if (bs)
+                c->pool->run((m + sl - 1) / sl, [=](unsigned k) {
+                    const uint32_t a = k * sl, b = a + sl < m ? a + sl : m;
+                    for (uint32_t j = a; j < b; ++j)
+                        out_off[s0 + j] += bs;
+                });
+            base += tot[i];
+            return QHUFF_OK;
+        }
         c->pool->copy(out + base, H + o_out + ob[i], tot[i]);
         const uint32_t *ho = (const uint32_t *) (H + o_oo) + s0 + i;
         const uint32_t bs = (uint32_t) base;
@@ -1361,6 +1488,10 @@ host_batch(qhuff_ctx *c, bool enc, const uint8_t *in, const uint32_t *in_off,
         base = sync->base_of(shard);
         if (base == ~0ull)
             return QHUFF_EDEVICE;
+        if (dout && !small)
+            for (unsigned i = 0; i < K; ++i)
+                if ((rc = issue_out(i, base + obase[i])))
+                    return rc;
         for (unsigned i = 0; i < K; ++i)
             if ((rc = unstage(i)))
                 return rc;

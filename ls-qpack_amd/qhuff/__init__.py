@@ -39,7 +39,7 @@ EXPORTS = (
     "qhuff_timing_enable", "qhuff_timing_read", "qhuff_kernel_variant",
     "qhuff_dec_int", "qhuff_encode_batch_host_multi",
     "qhuff_decode_batch_host_multi", "qhuff_encode_batch_multi",
-    "qhuff_decode_batch_multi",
+    "qhuff_decode_batch_multi", "qhuff_host_register", "qhuff_host_unregister",
     # include/qhuff_lsqpack.h
     "qhuff_lsqpack_enc_enc_str", "qhuff_lsqpack_huff_decode",
     "qhuff_lsqpack_set_decode_full", "qhuff_lsqpack_set_device",
@@ -238,6 +238,10 @@ def lib():
         L.qhuff_decode_batch_multi.restype = C.c_int
         L.qhuff_decode_batch_multi.argtypes = [vp, C.c_uint32, vp, vp,
                                                C.c_int]
+        L.qhuff_host_register.restype = C.c_int
+        L.qhuff_host_register.argtypes = [vp, C.c_size_t]
+        L.qhuff_host_unregister.restype = C.c_int
+        L.qhuff_host_unregister.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -373,6 +377,41 @@ def lsqpack_set_decode_full(fn):
 def _ctx_array(codecs):
     arr = (C.c_void_p * len(codecs))(*[c._ctx.value for c in codecs])
     return arr
+
+
+def host_register(arr):
+    """qhuff_host_register over a contiguous numpy array: the host-memory
+    calls then move it by DMA directly (no staging copy) -> rc."""
+    assert arr.flags["C_CONTIGUOUS"]
+    return int(lib().qhuff_host_register(_np_ptr(arr), arr.nbytes))
+
+
+def host_unregister(arr):
+    return int(lib().qhuff_host_unregister(_np_ptr(arr)))
+
+
+class registered:
+    """with registered(a, b, ...): the arrays are registered for direct DMA
+    inside the block (raises QhuffError if a registration fails)."""
+
+    def __init__(self, *arrays):
+        self.arrays = arrays
+        self.done = []
+
+    def __enter__(self):
+        for a in self.arrays:
+            rc = host_register(a)
+            if rc:
+                self.__exit__()
+                raise QhuffError("qhuff_host_register: %d %s"
+                                 % (rc, lib().qhuff_last_error(None).decode()))
+            self.done.append(a)
+        return self
+
+    def __exit__(self, *exc):
+        while self.done:
+            host_unregister(self.done.pop())
+        return False
 
 
 def encode_host_multi(codecs, data, in_off, mode=ENC_PAYLOAD):
