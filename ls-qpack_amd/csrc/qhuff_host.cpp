@@ -164,6 +164,9 @@ struct qhuff_ctx
                                          // larger launches use the device's
                                          // pool (slot_pool)
     bool pool_ref;                       // holds a reference on that pool
+    uint32_t max_banks;                  // pool banks it may open (1..4)
+    uint32_t pool_bank;                  // 1 + the pool bank its last full
+                                         // launch used (0: none yet)
     // kernel variant per kind (0 encode, 1 decode; pick_full): the full
     // kernel unless the batch is known (a hint) to need only the lean one
     bool last_full[2];                   // variant of the last launch
@@ -244,37 +247,49 @@ fail(qhuff_ctx *c, hipError_t e, const char *what)
 // wave, 151 MB for the resident grid of 256 CUs.  A launch of at most
 // kSmallGrid workgroups (the per-string entry points, small batches) uses a
 // region of its own context, allocated at its first such launch (4.7 MB);
-// larger ones share one pool per device, allocated at the first such launch
-// of any context and freed with the last context that used it.  So a
-// context's own device memory stays small (tables, look-back flags, its
-// staging), however many contexts a process opens.  Contexts order their
-// launches on the pool: the pool remembers the context and stream of its
-// last launch, and a launch of another context first records the pool's
-// event on that stream and waits for it (a context's own launches are
-// ordered by prepare_launch).  Nothing is recorded while one context uses
-// the pool -- an event record after every launch cost the bench line 4 %
-// (683-689 against 713-720 GB/s, profiles/r06_c) -- and a context that
-// joins a pool in use needs no device synchronisation, which would also
-// wait for other libraries' streams and a resident service kernel, under
-// the pool's lock (only if recording on the last launch's
-// stream fails, e.g. the caller destroyed it, is the device synchronised).
-// A pool outgrown by a larger grid is retired, not freed, until its last
-// user closes.  Launches of different contexts on the pool are serialised
-// this way even when they write no slot.
+// larger ones use one of the device's pool banks (up to kPoolBanks, each
+// allocated at its first use, all freed with the last context that used
+// the pool).  So a context's own device memory stays small (tables,
+// look-back flags, its staging), however many contexts a process opens.
+//
+// A bank belongs to the context of its last launch.  A context launches on
+// its own bank without any ordering (its own launches are ordered by
+// prepare_launch); a launch on a bank another context used last first
+// records the bank's event on that context's last stream and waits for it.
+// A context takes a bank from another only when it has none, or when no new
+// bank can be had: a context whose bank was taken from it (two contexts
+// alternating -- an encode stream and a decode stream) gets a bank of its
+// own, so concurrent contexts are not serialised; one context after another
+// (a second context opened later) reuses the first's bank.  Nothing is
+// recorded while a context keeps its bank -- an event record after every
+// launch cost the bench line 4 % (683-689 against 713-720 GB/s,
+// profiles/r06_c) -- and no device synchronisation is needed (it would also
+// wait for other libraries' streams and a resident service kernel, ADVICE
+// r05; only if recording on the last launch's stream fails, e.g. the caller
+// destroyed it, is the device synchronised).  A bank outgrown by a larger
+// grid is retired, not freed, until the pool's last user closes.
+// (QHUFF_SLOT_BANKS=1..4 caps the banks, read at qhuff_open; 1: every
+// context on one bank, the round-6 first design.)
 constexpr uint32_t kSmallGrid = 8;
 constexpr uint64_t kWaveSlotBytes = (uint64_t) kBigSlots * kBigSlotBytes;
 constexpr int kMaxDevices = 64;
+constexpr uint32_t kPoolBanks = 4;
+
+struct SlotBank
+{
+    uint8_t *p = nullptr;
+    uint64_t waves = 0;                  // slots for this many waves
+    hipEvent_t ev = nullptr;             // (recorded when it changes hands)
+    const qhuff_ctx *last_ctx = nullptr; // the last launch on it: its context
+    hipStream_t last_st = nullptr;       // and stream
+};
 
 struct SlotPool
 {
     std::mutex mu;
-    uint8_t *p = nullptr;
-    uint64_t waves = 0;                  // slots for this many waves
+    SlotBank bank[kPoolBanks];
     int refs = 0;                        // contexts that used it
-    hipEvent_t ev = nullptr;             // (recorded at a context switch)
-    const qhuff_ctx *last_ctx = nullptr; // the last launch on it: its context
-    hipStream_t last_st = nullptr;       // and stream
-    std::vector<uint8_t *> retired;      // outgrown pools (freed with it)
+    std::vector<uint8_t *> retired;      // outgrown banks (freed with it)
 };
 static SlotPool g_pool[kMaxDevices];
 
@@ -285,20 +300,22 @@ pool_release(int device, const qhuff_ctx *c)
         return;
     SlotPool &sp = g_pool[device];
     std::lock_guard<std::mutex> g(sp.mu);
-    if (sp.last_ctx == c)                // (its launches have completed)
-        sp.last_ctx = nullptr;
+    for (SlotBank &b : sp.bank)
+        if (b.last_ctx == c)             // (its launches have completed)
+            b.last_ctx = nullptr;
     if (--sp.refs > 0)
         return;
-    if (sp.p)
-        (void) hipFree(sp.p);
+    for (SlotBank &b : sp.bank)
+    {
+        if (b.p)
+            (void) hipFree(b.p);
+        if (b.ev)
+            (void) hipEventDestroy(b.ev);
+        b = SlotBank();
+    }
     for (uint8_t *q : sp.retired)
         (void) hipFree(q);
     sp.retired.clear();
-    if (sp.ev)
-        (void) hipEventDestroy(sp.ev);
-    sp.p = nullptr;
-    sp.waves = 0;
-    sp.ev = nullptr;
 }
 
 static uint64_t
@@ -307,6 +324,25 @@ max_grid_waves(const qhuff_ctx *c)
     const uint64_t e = (uint64_t) c->enc_grid * encode_waves_per_block();
     const uint64_t d = (uint64_t) c->dec_grid * decode_waves_per_block();
     return e > d ? e : d;
+}
+
+// the bank context c launches on (sp.mu held): its own; else a free one
+// (never used, or its context closed); else, if c's bank was taken from it,
+// a new one (up to c->max_banks); else the one c had, or bank 0
+static uint32_t
+pool_pick(SlotPool &sp, const qhuff_ctx *c)
+{
+    const uint32_t own = c->pool_bank;
+    if (own && (sp.bank[own - 1].last_ctx == c || !sp.bank[own - 1].last_ctx))
+        return own - 1;
+    for (uint32_t i = 0; i < c->max_banks; ++i)
+        if (sp.bank[i].p && !sp.bank[i].last_ctx)
+            return i;
+    if (own || !sp.bank[0].p)
+        for (uint32_t i = 0; i < c->max_banks; ++i)
+            if (!sp.bank[i].p)
+                return i;
+    return own ? own - 1 : 0;
 }
 
 // Runs launch(slots) for a launch of `grid` workgroups of `wpb` waves: the
@@ -350,47 +386,65 @@ with_slots(qhuff_ctx *c, uint32_t grid, uint64_t wpb, bool *full,
         c->pool_ref = true;
     }
     const uint64_t need = (uint64_t) grid * wpb;
-    if (sp.waves < need)
+    uint32_t bi = pool_pick(sp, c);
+    if (!sp.bank[bi].p && bi != 0 && sp.bank[0].p)
     {
-        if (sp.p)
+        // a new bank for a context whose bank was taken: if it cannot be
+        // had, share (the ordering below), never the lean kernel
+        const uint64_t mw = max_grid_waves(c);
+        const uint64_t w = mw > need ? mw : need;
+        if (hipMalloc((void **) &sp.bank[bi].p, w * kWaveSlotBytes) == hipSuccess)
+            sp.bank[bi].waves = w;
+        else
+        {
+            sp.bank[bi].p = nullptr;
+            (void) hipGetLastError();
+            bi = c->pool_bank ? c->pool_bank - 1 : 0;
+        }
+    }
+    SlotBank &b = sp.bank[bi];
+    if (b.waves < need)
+    {
+        if (b.p)
         {
             // (a grid larger than any seen: launches still running on the
-            // old pool keep it until the pool's last user closes)
-            sp.retired.push_back(sp.p);
-            sp.p = nullptr;
-            sp.waves = 0;
+            // old bank keep it until the pool's last user closes)
+            sp.retired.push_back(b.p);
+            b.p = nullptr;
+            b.waves = 0;
         }
         const uint64_t mw = max_grid_waves(c);
         const uint64_t w = mw > need ? mw : need;
-        if (hipMalloc((void **) &sp.p, w * kWaveSlotBytes) != hipSuccess)
+        if (hipMalloc((void **) &b.p, w * kWaveSlotBytes) != hipSuccess)
         {
-            sp.p = nullptr;
+            b.p = nullptr;
             (void) hipGetLastError();
             *full = false;
             return launch((uint8_t *) nullptr);
         }
-        sp.waves = w;
+        b.waves = w;
     }
-    if (sp.last_ctx && sp.last_ctx != c)
+    if (b.last_ctx && b.last_ctx != c)
     {
-        // after the pool's last launch, another context's: everything on
+        // after the bank's last launch, another context's: everything on
         // its stream so far
-        if (!sp.ev)
-            HIPCHK(c, hipEventCreateWithFlags(&sp.ev, hipEventDisableTiming));
-        hipError_t e = hipEventRecord(sp.ev, sp.last_st);
+        if (!b.ev)
+            HIPCHK(c, hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(b.ev, b.last_st);
         if (e == hipSuccess)
-            e = hipStreamWaitEvent(st, sp.ev, 0);
+            e = hipStreamWaitEvent(st, b.ev, 0);
         if (e != hipSuccess)
         {
             (void) hipGetLastError();
             HIPCHK(c, hipDeviceSynchronize());
         }
     }
-    const int rc = launch(sp.p);
+    const int rc = launch(b.p);
     if (rc == QHUFF_OK)
     {
-        sp.last_ctx = c;
-        sp.last_st = st;
+        b.last_ctx = c;
+        b.last_st = st;
+        c->pool_bank = bi + 1;
     }
     return rc;
 }
@@ -485,6 +539,13 @@ qhuff_open(int device, qhuff_ctx **ctx_out)
     }
     c->epoch = 0;
     c->hint[0] = c->hint[1] = -1;
+    c->max_banks = kPoolBanks;
+    if (const char *sb = getenv("QHUFF_SLOT_BANKS"))
+    {
+        const uint32_t k = (uint32_t) strtoul(sb, nullptr, 0);
+        if (k >= 1 && k <= kPoolBanks)
+            c->max_banks = k;
+    }
     {
         // tuning override: fewer workgroups per CU than fit
         const char *g = getenv("QHUFF_GRID_WG_PER_CU");

@@ -154,9 +154,12 @@ def test_two_contexts_concurrent_small(n):
 
 
 @pytest.mark.gpu
-def test_two_contexts_share_slot_pool_big_tiles():
-    """both contexts WRITE the device's shared big-tile slot
-    pool at once (qhuff_host.cpp with_slots).  The batch is the reference's
+@pytest.mark.parametrize("banks", ["1", "4"])
+def test_two_contexts_share_slot_pool_big_tiles(banks):
+    """both contexts WRITE the device's big-tile slot pool at
+    once (qhuff_host.cpp with_slots): with one bank (QHUFF_SLOT_BANKS=1)
+    they share it, ordered by its event; with four the second context takes
+    the first's bank once (ordered), then the first gets a bank of its own.  The batch is the reference's
     QIF corpora (tiles whose 1,461-byte values overflow the 3 KB stages)
     with a 4 KB string every 5,000 strings, 400k strings (~2 grid rounds)
     -- full kernels pinned, so every launch codes big tiles through the
@@ -180,15 +183,17 @@ def test_two_contexts_share_slot_pool_big_tiles():
     h, ho = O.encode_batch(data, off, 0)
     sh = workload.tile_shares(data, off, ho)
     assert sh["decode_slow_tile_share"] > 0 and sh["encode_slow_tile_share"] > 0
-    old = os.environ.get("QHUFF_KERNELS")
-    os.environ["QHUFF_KERNELS"] = "full"
+    env = {"QHUFF_KERNELS": "full", "QHUFF_SLOT_BANKS": banks}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         c1, c2 = qhuff.Codec(0), qhuff.Codec(0)
     finally:
-        if old is None:
-            del os.environ["QHUFF_KERNELS"]
-        else:
-            os.environ["QHUFF_KERNELS"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     d = _dev(data, torch)
     o = _dev(off.view(np.int32), torch)

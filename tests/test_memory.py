@@ -34,6 +34,13 @@ def test_per_string_contexts_small():
     rng = random.Random(4)
     strs = [bytes(rng.choice(b"abcdefgh-/.") for _ in range(rng.randrange(1, 60)))
             for _ in range(40)]
+    # (and the host path, on two contexts: six streams, so the runtime's
+    # hardware queues -- GPU_MAX_HW_QUEUES, device memory of their own that
+    # later streams share -- exist before the measurement, whichever tests
+    # ran before this one)
+    warm2 = qhuff.Codec(0)
+    for w in (warm, warm2):
+        w.encode_host(*_pack(strs), 0)
     before = free_bytes()
     ctxs = [qhuff.Codec(0) for _ in range(16)]
     try:
@@ -54,6 +61,7 @@ def test_per_string_contexts_small():
         for c in ctxs:
             c.close()
         warm.close()
+        warm2.close()
 
 
 def _pack(strs):
@@ -105,3 +113,42 @@ def test_token_batch_contexts_share_slots():
             second.close()
     finally:
         first.close()
+
+
+@pytest.mark.gpu
+def test_alternating_contexts_get_own_banks():
+    """Two contexts alternating full-grid launches (an encode stream and a
+    decode stream): the second takes the first's pool bank once, then the
+    first gets a bank of its own (one grid's slots, 48 KB a wave), so the
+    two are not serialised on one bank; outputs exact throughout."""
+    import qhuff
+    data, off = qhuff.synth_batch(1 << 19, seed=3)
+    h, ho = O.encode_batch(data, off, 0)
+    n = len(off) - 1
+    d_in = torch.from_numpy(data).cuda()
+    d_off = torch.from_numpy(off.view(np.int32)).cuda()
+    out = torch.empty(qhuff.encode_bound(len(data), n), dtype=torch.uint8,
+                      device="cuda")
+    oo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+
+    def run(c):
+        c.encode_into(d_in, d_off, n, 0, out, oo)
+        torch.cuda.synchronize()
+        assert np.array_equal(oo.cpu().numpy().view(np.uint32), ho)
+        assert np.array_equal(out[:int(ho[-1])].cpu().numpy(), h[:ho[-1]])
+
+    a, b = qhuff.Codec(0), qhuff.Codec(0)
+    try:
+        run(a)
+        run(b)                            # takes a's bank: no new memory
+        before = free_bytes()
+        for _ in range(3):
+            run(a)                        # a's bank was taken: a new one
+            run(b)
+        used = before - free_bytes()
+        props = torch.cuda.get_device_properties(0)
+        bank = props.multi_processor_count * 12 * 48 * 1024
+        assert bank * 0.9 <= used <= bank + 16 * MB, (used / MB, bank / MB)
+    finally:
+        a.close()
+        b.close()

@@ -35,7 +35,9 @@ python tools/pmc_summary.py $o/fetch $o/write 1048576 $o/pmc.json > /dev/null &&
 echo "== SQ"
 bash tools/sq_pass.sh $o/sq > $o/sq.txt 2>&1; tail -30 $o/sq.txt
 echo "== phases"
-TIMELINE=1 SLOW=1 RAW=$o/raw.npz QHUFF_LIB=$PWD/ls-qpack_amd/libqhuff_prof.so \
+# (the lean kernels by default: the profile build's stamps perturb the full
+# decode kernel's register allocation; PHASE_KERNELS=full for those)
+QHUFF_KERNELS=${PHASE_KERNELS:-lean} TIMELINE=1 SLOW=1 RAW=$o/raw.npz QHUFF_LIB=$PWD/ls-qpack_amd/libqhuff_prof.so \
     timeout -k 10 240 python -u tools/profile_phases.py > $o/phases.txt 2>&1
 rc=$?; fatal $rc
 python tools/wave_report.py $o/raw.npz > $o/wave_report.txt 2>&1
