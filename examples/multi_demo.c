@@ -85,12 +85,38 @@ main(int argc, char **argv)
         bad += st[i] != QHUFF_DEC_OK;
     bad += memcmp(doff, off, 4 * ((size_t) n + 1)) != 0
          || memcmp(dec, data, raw) != 0;
+    /* the same calls again on registered buffers (qhuff_host_register):
+     * DMA straight from / into them, the same results */
+    uint8_t *dec2 = malloc(db), *st2 = malloc(n);
+    uint32_t *doff2 = malloc(4 * ((size_t) n + 1));
+    void *reg[] = {data, off, enc1, eoff1, dec2, doff2, st2};
+    const size_t regb[] = {raw ? raw : 1, 4 * ((size_t) n + 1), eb,
+                           4 * ((size_t) n + 1), db, 4 * ((size_t) n + 1), n};
+    for (int k = 0; k < 7; ++k)
+        if (qhuff_host_register(reg[k], regb[k]) != QHUFF_OK)
+        {
+            fprintf(stderr, "qhuff_host_register: %s\n", qhuff_last_error(NULL));
+            return 1;
+        }
+    rc = qhuff_encode_batch_host_multi(ctx, g, data, off, n, QHUFF_ENC_PAYLOAD,
+                                       enc1, eoff1);
+    rc1 = qhuff_decode_batch_host_multi(ctx, g, enc1, eoff1, n, dec2, doff2, st2);
+    for (int k = 0; k < 7; ++k)
+        qhuff_host_unregister(reg[k]);
+    if (rc || rc1)
+    {
+        fprintf(stderr, "registered: %d / %d\n", rc, rc1);
+        return 1;
+    }
+    bad += memcmp(eoff1, eoff, 4 * ((size_t) n + 1)) != 0
+         || memcmp(enc1, enc, hb) != 0 || memcmp(doff2, doff, 4 * ((size_t) n + 1)) != 0
+         || memcmp(dec2, dec, raw) != 0 || memcmp(st2, st, n) != 0;
     printf("multi_demo: %u contexts on %d device(s), %u strings, %llu raw / "
-           "%u Huffman bytes, mismatches %ld\n", g, ndev, n,
-           (unsigned long long) raw, hb, bad);
+           "%u Huffman bytes, mismatches %ld (staged and registered)\n", g,
+           ndev, n, (unsigned long long) raw, hb, bad);
     for (uint32_t k = 0; k < g; ++k)
         qhuff_close(ctx[k]);
     free(data); free(off); free(enc); free(enc1); free(eoff); free(eoff1);
-    free(dec); free(st); free(doff);
+    free(dec); free(st); free(doff); free(dec2); free(st2); free(doff2);
     return bad ? 1 : 0;
 }

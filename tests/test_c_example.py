@@ -98,13 +98,16 @@ def test_multi_demo_builds_and_links():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("g", [1, 2, 3])
-def test_multi_demo_round_trip(g):
+@pytest.mark.parametrize("g,n", [(1, 100003), (2, 100003), (3, 100003),
+                                 (1, 600011), (3, 600011)])
+def test_multi_demo_round_trip(g, n):
     """qhuff_encode_batch_host_multi / qhuff_decode_batch_host_multi from a
     plain C99 caller: G contexts (round-robin over the visible devices),
     the stitched encode equals a one-context encode byte for byte and the
-    stitched decode equals the input"""
-    r = subprocess.run([MULTI, str(g), "100003"], capture_output=True,
+    stitched decode equals the input; then both again on buffers registered
+    with qhuff_host_register (600k strings: several staging chunks a shard,
+    so the outputs come back by direct DMA), the same bytes"""
+    r = subprocess.run([MULTI, str(g), str(n)], capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "mismatches 0" in r.stdout
+    assert "mismatches 0 (staged and registered)" in r.stdout
