@@ -1,7 +1,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-o=gpurun_out/r06_q; mkdir -p $o
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $o/pytest.log 2>&1 || { tail -40 $o/pytest.log; exit 1; }
-tail -2 $o/pytest.log
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 > $o/bench2.json 2> $o/bench2.err
-tail -c 700 $o/bench2.json
+for L in 3 2 4; do
+  if [ $L = 3 ]; then unset NOTEST; else export NOTEST=1; fi
+  BASE=libqhuff.so REPS=2 WORKLOADS="corpus" timeout -k 10 600 bash tools/ab_cand.sh r06_late/l$L libqhuff_l$L.so > gpurun_out/r06_late_l$L.txt 2>&1 || { cat gpurun_out/r06_late_l$L.txt; exit 1; }
+  echo "== L=$L"; cat gpurun_out/r06_late_l$L.txt
+done
