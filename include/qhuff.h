@@ -142,10 +142,10 @@ int qhuff_decode_batch_host(qhuff_ctx *ctx, const uint8_t *in,
 
 /* (ABI 7) Register caller buffers for direct DMA by the host-memory calls
  * (hipHostRegister, portable to every device; process-wide).  When a host
- * call's input bytes and offsets lie in registered ranges they are
- * transferred to the device directly, without the pinned staging copy; when
- * its output buffer (the bound), offsets and statuses do, the results are
- * transferred straight into them.  Register long-lived buffers once (it pins
+ * call's input bytes and offsets each lie within one registered range they
+ * are transferred to the device directly, without the pinned staging copy;
+ * when its output buffer (the bound), offsets and statuses do, the results
+ * are transferred straight into them (batches past one 4 MB staging chunk).  Register long-lived buffers once (it pins
  * their pages: milliseconds for tens of MB); the results are the same either
  * way.  qhuff_host_register: QHUFF_OK, QHUFF_EINVAL (null, 0 bytes, or ptr
  * already registered), QHUFF_ENOMEM / QHUFF_EDEVICE (the reason in
