@@ -136,3 +136,20 @@ def test_registered_multi(codecs, token, g):
                                                p(qo), p(st)) == qhuff.OK
         assert not st[:n].any()
         assert np.array_equal(qo, o) and np.array_equal(q[:qo[-1]], d)
+
+
+@pytest.mark.gpu
+def test_registered_too_small_is_staged(codecs, token):
+    """an output buffer registered with fewer bytes than the call's bound
+    (here exactly the output) is not used for direct DMA: the call stages
+    as before, same bytes"""
+    d, o, h, ho = token
+    n = len(o) - 1
+    c = codecs[0]
+    bound = qhuff.encode_bound(int(o[-1]), n, 0)
+    e = np.zeros(bound, dtype=np.uint8)
+    eo = np.zeros(n + 1, dtype=np.uint32)
+    part = e[:int(ho[-1])]
+    with qhuff.registered(d, o, part, eo):
+        e2, eo2 = c.encode_host(d, o, 0, out=e, out_off=eo)
+    assert np.array_equal(eo2, ho) and np.array_equal(e2, h)
