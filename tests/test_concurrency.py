@@ -225,3 +225,66 @@ def test_two_contexts_share_slot_pool_big_tiles(banks):
         assert np.array_equal(do[:len(data)].cpu().numpy(), data)
     c1.close()
     c2.close()
+
+
+@pytest.mark.gpu
+def test_more_contexts_than_pool_banks():
+    """five contexts on five streams, full kernels, big tiles, launches in
+    rotation: four get pool banks of their own, the fifth (past the cap of
+    four) takes banks from the others, ordered by their events -- every
+    output bit-exact, no device error"""
+    import os
+    import random
+    import torch
+    import qhuff
+    from qhuff import workload
+    here = os.path.dirname(os.path.abspath(__file__))
+    data, off = workload.corpus_batch(200_000,
+                                      os.path.join(here, "golden", "data"))
+    strs = [bytes(data[off[i]:off[i + 1]]) for i in range(len(off) - 1)]
+    rng = random.Random(9)
+    for i in range(0, len(strs), 4000):
+        strs[i] = bytes(rng.choice(b"klmnopq-_/") for _ in range(4096))
+    data, off = workload.pack(strs)
+    n = len(off) - 1
+    h, ho = O.encode_batch(data, off, 0)
+    old = os.environ.get("QHUFF_KERNELS")
+    os.environ["QHUFF_KERNELS"] = "full"
+    try:
+        cs = [qhuff.Codec(0) for _ in range(5)]
+    finally:
+        if old is None:
+            del os.environ["QHUFF_KERNELS"]
+        else:
+            os.environ["QHUFF_KERNELS"] = old
+    ss = [torch.cuda.Stream() for _ in cs]
+    d = _dev(data, torch)
+    o = _dev(off.view(np.int32), torch)
+    hd = _dev(h, torch)
+    hod = _dev(ho.view(np.int32), torch)
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(2):
+        for c, s in zip(cs, ss):
+            eo = torch.empty(qhuff.encode_bound(len(data), n, 0),
+                             dtype=torch.uint8, device="cuda")
+            eoo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+            do = torch.empty(qhuff.decode_bound(len(h), n), dtype=torch.uint8,
+                             device="cuda")
+            doo = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+            st = torch.empty(n, dtype=torch.uint8, device="cuda")
+            c.encode_into(d, o, n, 0, eo, eoo, s)
+            c.decode_into(hd, hod, n, do, doo, st, s)
+            outs.append((eo, eoo, do, doo, st))
+    torch.cuda.synchronize()
+    for c in cs:
+        assert c.device_error() == 0
+    for eo, eoo, do, doo, st in outs:
+        eoo = eoo.cpu().numpy().view(np.uint32)
+        assert np.array_equal(eoo, ho)
+        assert np.array_equal(eo[:int(eoo[-1])].cpu().numpy(), h)
+        assert np.array_equal(doo.cpu().numpy().view(np.uint32), off)
+        assert not st.cpu().numpy().any()
+        assert np.array_equal(do[:len(data)].cpu().numpy(), data)
+    for c in cs:
+        c.close()

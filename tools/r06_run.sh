@@ -1,4 +1,5 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-BASE=libqhuff.so REPS=3 WORKLOADS="corpus" timeout -k 10 800 bash tools/ab_cand.sh r06_ei libqhuff_ei.so > gpurun_out/r06_ei.txt 2>&1 || { cat gpurun_out/r06_ei.txt; exit 1; }
-grep -v amdgpu.ids gpurun_out/r06_ei.txt
+o=gpurun_out/r06_r; mkdir -p $o
+timeout -k 10 300 python -u -m pytest tests/test_concurrency.py tests/test_memory.py -x -v --timeout 120 --timeout-method thread > $o/pytest.log 2>&1 || { tail -40 $o/pytest.log; exit 1; }
+tail -3 $o/pytest.log
