@@ -153,6 +153,18 @@ def test_gpu_headers_random(codec, kind):
 
 
 @pytest.mark.gpu
+def test_gpu_headers_several_rounds(codec):
+    """1M headers (16,384 tiles): more tiles than the resident grid has
+    waves, so each persistent wave hashes two or three tiles through its
+    prefetch loop (the synthetic case above fits one round)"""
+    import qhuff
+    data, off = qhuff.synth_batch(2 * (1 << 20), seed=123)
+    g1, g2 = gpu_headers(codec, data, off)
+    o1, o2 = O.xxh32_headers(data, off)
+    assert np.array_equal(g1, o1) and np.array_equal(g2, o2)
+
+
+@pytest.mark.gpu
 def test_gpu_zero_headers(codec):
     g1, g2 = gpu_headers(codec, np.zeros(0, dtype=np.uint8),
                          np.zeros(1, dtype=np.uint32))
